@@ -1,0 +1,176 @@
+/*
+ * flipwalk.h — C-ABI of the MI355X-native batched single-node flip walk.
+ *
+ * This is the drop-in boundary for the one hot path of
+ * drdeford/FlipComplexityEmpirical: GerryChain's
+ *
+ *   MarkovChain(proposal, Validator([single_flip_contiguous, popbound]),
+ *               accept=cut_accept, initial_state, total_steps)
+ *
+ * as constructed at grid_chain_sec11.py:340-342 (also All_States_Chain.py:300-302,
+ * Frankenstein_chain.py:370-372) and iterated at grid_chain_sec11.py:366.
+ * The reference has no FFI of its own (it is pure Python over GerryChain); the
+ * entry points below are what a ctypes binding of that loop binds.  Each one
+ * names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Return 0 on success, a negative FW_E* code on error; fw_last_error() gives
+ *    a thread-local message.
+ *  - Host buffers are owned by the caller and copied in/out.  Device memory is
+ *    owned by the library behind the opaque handles.
+ *  - One handle is bound to one HIP device; calls on one handle must be
+ *    serialised; different handles may be driven from different host threads.
+ *  - Graphs are CSR with strictly ascending neighbour lists, no self loops, and
+ *    symmetric adjacency (checked by fw_graph_create).  Node ids 0..n-1.
+ *  - District labels are 0..k-1 (the façade maps GerryChain labels such as
+ *    ±1 onto them in sorted order).
+ *
+ * Randomness (a deterministic restatement of the reference's unseeded
+ * `random.choice` / `random.random`, grid_chain_sec11.py:143,179): proposal
+ * attempt t of global chain g draws ONE Philox4x32-10 block
+ *     key = (lo32(seed), hi32(seed)),  ctr = (lo32(t), hi32(t), lo32(g), hi32(g))
+ * giving words x0..x3.  The proposal takes the r-th element, r =
+ * floor(((x1<<32)|x0) * P / 2^64), of the proposal set in canonical order (P =
+ * its size); the Metropolis draw is CPython's random() construction
+ * u = ((x2>>5)*2^26 + (x3>>6)) * 2^-53.
+ */
+#ifndef FLIPWALK_H
+#define FLIPWALK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ---------------------------------------------------------- */
+#define FW_OK 0
+#define FW_EINVAL (-1)      /* bad argument / malformed graph                */
+#define FW_EHIP (-2)        /* HIP runtime error                             */
+#define FW_ESTATE (-3)      /* invalid initial state (GerryChain ValueError) */
+#define FW_EUNSUPPORTED (-4)/* configuration outside what the kernels handle */
+#define FW_ENOMEM (-5)
+
+/* ---- proposal modes -------------------------------------------------------
+ * FW_PROPOSE_BI     slow_reversible_propose_bi  grid_chain_sec11.py:132-145
+ *                   uniform boundary node, flipped to the other label (k==2).
+ * FW_PROPOSE_PAIRS  slow_reversible_propose     grid_chain_sec11.py:117-130 with
+ *                   the pair updater b_nodes :151-153 — uniform over distinct
+ *                   (node, foreign-neighbour-label) pairs, ordered (node, label).
+ * FW_PROPOSE_CUTEDGE gerrychain.proposals.propose_random_flip (imported
+ *                   grid_chain_sec11.py:24): uniform cut edge, uniform
+ *                   endpoint == uniform directed cut edge (v,u) ordered (v,u);
+ *                   v takes u's label.                                        */
+#define FW_PROPOSE_BI 0
+#define FW_PROPOSE_PAIRS 1
+#define FW_PROPOSE_CUTEDGE 2
+
+/* ---- what fw_chains_read can return -------------------------------------- */
+#define FW_READ_LABELS 0   /* int16  [n_chains][n]                            */
+#define FW_READ_STATS 1    /* fw_chain_stats [n_chains]                       */
+#define FW_READ_HIST_CUT 2 /* uint64 [n_edges+1]  yields with |cut edges| = i */
+#define FW_READ_HIST_B 3   /* uint64 [n+1]        yields with |B| = i         */
+#define FW_READ_POPS 4     /* int64  [n_chains][k] district populations       */
+
+/* Per-chain counters and running observables (the per-yield block of
+ * grid_chain_sec11.py:366-402, reduced to sums; one struct per chain). */
+typedef struct fw_chain_stats {
+  uint64_t attempts;    /* proposals drawn, including invalid (retried) ones   */
+  uint64_t steps;       /* valid proposals = MarkovChain counter increments    */
+  uint64_t accepts;     /* Metropolis-accepted flips                           */
+  uint64_t pop_fail;    /* proposals rejected by the population bound          */
+  uint64_t contig_fail; /* proposals (pop-valid) rejected by contiguity        */
+  uint64_t bfs_runs;    /* contiguity checks that needed a graph search        */
+  uint64_t bfs_nodes;   /* nodes dequeued by those searches                    */
+  uint64_t bfs_deg;     /* sum of degrees of dequeued nodes                    */
+  uint64_t sum_deg;     /* sum over proposals of deg(v)                        */
+  uint64_t acc_deg;     /* sum over accepts of deg(v)                          */
+  uint64_t n_bchg;      /* nodes entering/leaving the boundary, over accepts   */
+  uint64_t yields;      /* yielded states counted (initial state included)     */
+  int64_t sum_cut;      /* sum over yields of len(cut_edges)   (rce, :367)     */
+  int64_t sum_bnodes;   /* sum over yields of len(b_nodes)     (rbn, :369)     */
+  double sum_invb;      /* sum over yields of 1/len(b_nodes); the expected
+                           geom wait (:147-148) is (N^k-1)*sum_invb - yields   */
+  int32_t cut;          /* current len(cut_edges)                              */
+  int32_t bnodes;       /* current number of boundary nodes                    */
+  int32_t npairs;       /* current size of the proposal set                    */
+  int32_t stuck;        /* 1 once max_retries consecutive proposals failed     */
+} fw_chain_stats;
+
+typedef struct fw_graph fw_graph;
+typedef struct fw_chains fw_chains;
+
+/* Thread-local description of the last error on this thread. */
+const char* fw_last_error(void);
+
+/* Library/ABI version, e.g. 0x000100 for 0.1.0. */
+int32_t fw_version(void);
+
+/* Number of visible HIP devices (0 when none; never fails). */
+int32_t fw_device_count(void);
+
+/* Upload a CSR graph (replaces gerrychain.Graph / networkx adjacency,
+ * grid_chain_sec11.py:191-260, All_States_Chain.py:221).  pop may be NULL
+ * (every node population 1, grid_chain_sec11.py:218).  Row-major W×H grids
+ * are detected and get an implicit-neighbour kernel. */
+int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
+                    int32_t n, int32_t nnz, int device, fw_graph** out);
+void fw_graph_destroy(fw_graph* g);
+/* info[0]=n, info[1]=n_edges, info[2]=maxdeg, info[3]=grid width (0 = not a grid),
+ * info[4]=grid height */
+int fw_graph_info(const fw_graph* g, int64_t info[5]);
+
+/* Create n_chains chains (replaces Partition(graph, assignment, updaters) +
+ * within_percent_of_ideal_population + MarkovChain.__init__'s validity check,
+ * grid_chain_sec11.py:316-342).
+ *  init_labels  int16 [1 or n_chains][n], values 0..k-1 (init_per_chain 0/1)
+ *  pop_lo/hi    integer population bounds ceil(lo), floor(hi) of Bounds
+ *  thr          float64 [1 or n_chains][2*maxdeg+1]; thr[d+maxdeg] is the
+ *               Metropolis bound base**(-d) for Δcut = d (cut_accept,
+ *               grid_chain_sec11.py:171-179), thr_per_chain 0/1
+ *  seed         Philox key; chain_id0 = global id of the first local chain
+ * Fails with FW_ESTATE when an initial plan is not contiguous or violates the
+ * bounds (GerryChain raises ValueError). */
+int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* init_labels,
+                     int32_t init_per_chain, int32_t proposal_mode, int64_t pop_lo,
+                     int64_t pop_hi, const double* thr, int32_t thr_per_chain, uint64_t seed,
+                     int64_t chain_id0, fw_chains** out);
+void fw_chains_destroy(fw_chains* c);
+
+/* Advance every chain by `steps` counted steps (MarkovChain.__next__ called
+ * `steps` times; the initial state is yielded once, on the first call).  A
+ * chain that draws max_retries consecutive invalid proposals is marked stuck
+ * instead of looping forever (the reference would hang).  Blocking. */
+int fw_chains_run(fw_chains* c, int64_t steps, int32_t max_retries);
+
+/* Same, asynchronous on the handle's stream; fw_chains_sync waits.  The last
+ * kernel's device time (ms, HIP events on that stream) is returned by
+ * fw_chains_last_kernel_ms. */
+int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries);
+int fw_chains_sync(fw_chains* c);
+double fw_chains_last_kernel_ms(const fw_chains* c);
+
+/* Copy a state array back to the host (see FW_READ_*). */
+int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes);
+
+/* Zero the per-chain sums and the yield histograms (not the chain states). */
+int fw_chains_reset_observables(fw_chains* c);
+
+/* Batched per-flip evaluation on ONE state — the bit-exact per-step contract
+ * (cut_edges updater, single_flip_contiguous, Bounds, b_nodes_bi):
+ * for each i < m, flipping v[i] to target[i] gives
+ *   dcut[i]      = len(cut_edges) after - before
+ *   contig[i]    = 1 iff the old district of v[i] stays connected and non-empty
+ *   pop_ok[i]    = 1 iff both changed districts stay inside [pop_lo, pop_hi]
+ *   dboundary[i] = number of boundary nodes after - before
+ * Flips with target == labels[v] or out-of-range values fail with FW_EINVAL. */
+int fw_eval_flips(fw_graph* g, const int16_t* labels, int32_t k, const int32_t* v,
+                  const int16_t* target, int32_t m, int64_t pop_lo, int64_t pop_hi,
+                  int32_t* dcut, uint8_t* contig, uint8_t* pop_ok, int32_t* dboundary);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLIPWALK_H */

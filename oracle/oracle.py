@@ -1,0 +1,142 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the C oracle (flipchain_oracle.c).
+
+Each function cites the reference behaviour it restates; see the C file header.
+Builds ``oracle/liboracle.so`` with ``make -C oracle`` when it is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+STATS_DTYPE = np.dtype(
+    [
+        ("attempts", "<u8"),
+        ("steps", "<u8"),
+        ("accepts", "<u8"),
+        ("pop_fail", "<u8"),
+        ("contig_fail", "<u8"),
+        ("bfs_runs", "<u8"),
+        ("bfs_nodes", "<u8"),
+        ("bfs_deg", "<u8"),
+        ("sum_deg", "<u8"),
+        ("acc_deg", "<u8"),
+        ("n_bchg", "<u8"),
+        ("yields", "<u8"),
+        ("sum_cut", "<i8"),
+        ("sum_bnodes", "<i8"),
+        ("sum_invb", "<f8"),
+        ("cut", "<i4"),
+        ("bnodes", "<i4"),
+        ("npairs", "<i4"),
+        ("stuck", "<i4"),
+    ]
+)
+
+_P = ctypes.c_void_p
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "flipchain_oracle.c")
+    if (not os.path.exists(path)) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        L = ctypes.CDLL(build())
+        L.orc_philox4x32_10.argtypes = [_P, _P, _P]
+        L.orc_philox4x32_10.restype = None
+        L.orc_scale64.argtypes = [ctypes.c_uint32] * 3
+        L.orc_scale64.restype = ctypes.c_uint32
+        L.orc_u53.argtypes = [ctypes.c_uint32] * 2
+        L.orc_u53.restype = ctypes.c_double
+        L.orc_run_chain.argtypes = [
+            _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+            ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_uint64, ctypes.c_uint64, _P, _P,
+            ctypes.c_int64, ctypes.c_int32, _P, _P, _P, _P,
+        ]
+        L.orc_run_chain.restype = ctypes.c_int
+        L.orc_eval_flips.argtypes = [
+            _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
+            ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P,
+        ]
+        L.orc_eval_flips.restype = ctypes.c_int
+        L.orc_plan_valid.argtypes = [
+            _P, _P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int64, ctypes.c_int64,
+        ]
+        L.orc_plan_valid.restype = ctypes.c_int
+        L.orc_stats_size.restype = ctypes.c_int32
+        assert L.orc_stats_size() == STATS_DTYPE.itemsize
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def philox4x32_10(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().orc_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
+    return out
+
+
+def new_stats(n=1):
+    return np.zeros(n, dtype=STATS_DTYPE)
+
+
+def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps,
+              max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False):
+    """Run one chain on the CPU oracle.  ``graph`` needs rowptr/col/pop/n/grid_w.
+
+    Returns (labels, stats, pops, trace-or-None); ``labels`` is a new int16 array.
+    """
+    lab = np.array(labels, dtype=np.int16, copy=True)
+    st = new_stats(1) if stats is None else stats
+    thr = np.ascontiguousarray(thr, dtype=np.float64)
+    tr = np.full(int(steps), -2, dtype=np.int32) if trace else None
+    pops = np.zeros(k, dtype=np.int64)
+    rc = lib().orc_run_chain(
+        _ptr(graph.rowptr), _ptr(graph.col), _ptr(graph.pop), graph.n, graph.grid_w, k, mode,
+        int(pop_lo), int(pop_hi), _ptr(thr), int(seed), int(chain_id), _ptr(lab), _ptr(st),
+        int(steps), int(max_retries), _ptr(hist_cut), _ptr(hist_b), _ptr(tr), _ptr(pops),
+    )
+    if rc != 0:
+        raise MemoryError("oracle allocation failed")
+    return lab, st, pops, tr
+
+
+def eval_flips(graph, labels, k, v, target, pop_lo, pop_hi):
+    lab = np.ascontiguousarray(labels, dtype=np.int16)
+    v = np.ascontiguousarray(v, dtype=np.int32)
+    t = np.ascontiguousarray(target, dtype=np.int16)
+    m = len(v)
+    dcut = np.zeros(m, np.int32)
+    contig = np.zeros(m, np.uint8)
+    pop_ok = np.zeros(m, np.uint8)
+    dbound = np.zeros(m, np.int32)
+    rc = lib().orc_eval_flips(
+        _ptr(graph.rowptr), _ptr(graph.col), _ptr(graph.pop), graph.n, graph.grid_w, k, _ptr(lab),
+        _ptr(v), _ptr(t), m, int(pop_lo), int(pop_hi), _ptr(dcut), _ptr(contig), _ptr(pop_ok),
+        _ptr(dbound),
+    )
+    if rc != 0:
+        raise MemoryError("oracle allocation failed")
+    return dcut, contig, pop_ok, dbound
+
+
+def plan_valid(graph, labels, k, pop_lo, pop_hi):
+    lab = np.ascontiguousarray(labels, dtype=np.int16)
+    return bool(lib().orc_plan_valid(_ptr(graph.rowptr), _ptr(graph.col), _ptr(graph.pop),
+                                     graph.n, k, _ptr(lab), int(pop_lo), int(pop_hi)))
