@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""bench.py — flip steps/sec of the batched single-node flip walk on MI355X.
+
+Workload (BASELINE.json configs[2], SURVEY.md §8d "C3"): 100x100 grid, k=4 districts
+seeded as 50x50 quadrants, 65,536 independent chains per GPU, proposal
+slow_reversible_propose over (node, foreign label) pairs (grid_chain_sec11.py:117-130),
+single_flip_contiguous + 5% population bound, Metropolis cut_accept with base
+mu = 2.63815853 (grid_chain_sec11.py:33,171-179).
+
+A bench "step" is one kernel launch that advances every chain by --inner counted flip
+steps (valid proposals, MarkovChain counter increments); value = counted flip steps of
+all chains on all ranks / max-over-ranks wall time of the K timed launches.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Extra fields: "roofline" (dominant kernel, algorithmic bytes of SURVEY.md §8d per launch /
+mean HIP-event launch time vs 8 TB/s) and "cpu_baseline" (the GerryChain-equivalent
+Python proxy, oracle/reference_proxy.py, one chain per process on the host cores, rank 0
+at N=1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MU = 2.63815853
+METRIC = "flip steps/sec (whole node), 100×100 grid k=4 batched chains; % HBM peak"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(d):
+    """SURVEY.md §8d byte model over counter deltas ``d`` (int32 CSR, int16 labels).
+
+    B_prop = 30 + 6*d_v + sum over dequeued search nodes (8 + 6*d_u)
+    B_acc  = 10 + 2*(1 + d_v) + 12*n_bchg
+    """
+    return (30 * d["attempts"] + 6 * d["sum_deg"] + 8 * d["bfs_nodes"] + 6 * d["bfs_deg"]
+            + 12 * d["accepts"] + 2 * d["acc_deg"] + 12 * d["n_bchg"])
+
+
+def totals(st):
+    keys = ["attempts", "steps", "accepts", "pop_fail", "contig_fail", "bfs_runs", "bfs_nodes",
+            "bfs_deg", "sum_deg", "acc_deg", "n_bchg"]
+    return {k: int(st[k].astype(np.uint64).sum()) for k in keys}
+
+
+# ------------------------------------------------------------------ CPU baseline
+def _proxy_worker(args):
+    n, k, percent, base, seed, cid, seconds = args
+    sys.path.insert(0, ROOT)
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    from oracle.reference_proxy import ProxyChain
+    g = grid_graph(n, n)
+    lab = block_seed(n, n, 2, 2)
+    ch = ProxyChain(g, lab, k, 1, percent, base, seed, cid)
+    ch.run(1)  # builds caches
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < seconds:
+        ch.run(5)
+        steps += 5
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(n, k, percent, base, seed, seconds=10.0, workers=None):
+    workers = workers or min(16, os.cpu_count() or 1)
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_proxy_worker, [(n, k, percent, base, seed, i, seconds)
+                                       for i in range(workers)])
+    rate = sum(s / t for s, t in res)
+    return {"value": rate, "unit": "flip steps/s", "cores": workers, "kind": "port",
+            "sample": f"GerryChain-equivalent Python proxy (oracle/reference_proxy.py): "
+                      f"{workers} chains x ~{seconds:.0f}s, one chain per process, same C3 "
+                      f"config ({n}x{n} grid, k={k}, pairs proposal, base {base}, "
+                      f"{percent:.0%} pop); {sum(s for s, _ in res)} steps total"}
+
+
+def native_cpu_rate(n, k, percent, base, seed, steps=20000):
+    from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    from oracle import oracle as O
+    g = grid_graph(n, n)
+    lo, hi = population_bounds(g.total_pop, k, percent)
+    t0 = time.perf_counter()
+    O.run_chain(g, block_seed(n, n, 2, 2), k, 1, lo, hi, metropolis_table(base, g.maxdeg), seed,
+                0, steps)
+    return steps / (time.perf_counter() - t0)
+
+
+# ------------------------------------------------------------------ main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--inner", type=int, default=1000, help="flip steps per chain per launch")
+    ap.add_argument("--chains", type=int, default=65536, help="chains per GPU (weak scaling)")
+    ap.add_argument("--grid", type=int, default=100)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--base", type=float, default=MU)
+    ap.add_argument("--percent", type=float, default=0.05)
+    ap.add_argument("--proposal", default="pairs")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM bytes from a rocprofv3 PMC pass (profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bounds
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    from flipcomplexityempirical_amd.distributed import merge_histograms
+
+    n, k = args.grid, args.k
+    g = grid_graph(n, n)
+    init = block_seed(n, n, 2, 2) if k == 4 else block_seed(n, n, 2, k // 2)
+    bounds = population_bounds(g.total_pop, k, args.percent)
+    dg = DeviceGraph(g, device=local_rank)
+    ch = Chains(dg, args.chains, k, init, proposal=args.proposal, pop_bounds=bounds, base=args.base,
+                seed=args.seed, chain_id0=rank * args.chains)
+
+    def barrier():
+        torch.cuda.synchronize(local_rank)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(local_rank)
+
+    for _ in range(args.warmup):
+        ch.run(args.inner)
+    st0 = totals(ch.stats())
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        ch.run_async(args.inner)
+        ch.sync()
+        kms.append(ch.last_kernel_ms())
+    barrier()
+    dt = time.perf_counter() - t0
+    st1_arr = ch.stats()
+    st1 = totals(st1_arr)
+    d = {kk: st1[kk] - st0[kk] for kk in st1}
+    steps_local = d["steps"]
+    if dist is not None:
+        t = torch.tensor([dt, float(steps_local)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        dt, steps_all = float(t[0]), float(t[1])
+    else:
+        steps_all = float(steps_local)
+    hist_cut, hist_b = merge_histograms(ch.hist_cut(), ch.hist_b(), dist)
+
+    kernel_ms = float(np.mean(kms))
+    bytes_per_launch = algorithmic_bytes(d) / args.steps
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": steps_all / dt,
+            "unit": "flip steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"C3: {n}x{n} grid, k={k} quadrant seed, {args.chains} chains/GPU, "
+                            f"{args.proposal} proposal, base {args.base}, "
+                            f"{args.percent:.0%} pop bound, contiguity",
+                "chains_per_gpu": args.chains,
+                "flip_steps_per_chain_per_step": args.inner,
+                "parallelism": f"chains sharded over {world} GPU(s), RCCL histogram merge",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+            },
+            "kernel_ms": kernel_ms,
+            "proposals_per_s": d["attempts"] * world / dt,
+            "accepts_per_s": d["accepts"] * world / dt,
+            "valid_frac": d["steps"] / max(1, d["attempts"]),
+            "accept_frac": d["accepts"] / max(1, d["steps"]),
+            "bfs_runs_per_step": d["bfs_runs"] / max(1, d["steps"]),
+            "bfs_nodes_per_run": d["bfs_nodes"] / max(1, d["bfs_runs"]),
+            "alg_bytes_per_proposal": algorithmic_bytes(d) / max(1, d["attempts"]),
+            "mean_cut": float(st1_arr["cut"].mean()),
+            "mean_bnodes": float(st1_arr["bnodes"].mean()),
+            "hist_yields": int(hist_cut.sum()),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n, k, args.percent, args.base, args.seed,
+                                               seconds=args.cpu_seconds)
+            out["cpu_native_1core"] = native_cpu_rate(n, k, args.percent, args.base, args.seed)
+        print(json.dumps(out), flush=True)
+    ch.close()
+    dg.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,229 @@
+"""Batched flip-walk chains on MI355X (host side of the drop-in boundary).
+
+``Chains`` is the batched form of the reference's
+
+    MarkovChain(slow_reversible_propose_bi, Validator([single_flip_contiguous, popbound]),
+                accept=cut_accept, initial_state=grid_partition, total_steps=100000)
+
+(grid_chain_sec11.py:340-342): thousands of independent chains, one per Philox
+stream, advanced by the HIP kernel through the C-ABI.  Host-side numerics that
+the kernels take as inputs are computed here exactly as the reference computes
+them in Python:
+
+* ``population_bounds`` — ``within_percent_of_ideal_population`` (grid_chain_sec11.py:319):
+  ideal = sum(pops)/k, (1-p)*ideal <= pop <= (1+p)*ideal with Python floats, turned
+  into the equivalent integer interval [ceil(lo), floor(hi)].
+* ``metropolis_table`` — ``cut_accept`` (grid_chain_sec11.py:171-179): bound =
+  base ** (len(parent cut) - len(cut)) = base ** (-Δcut) with Python's float pow.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import STATS_DTYPE, check, ptr
+from .graph import Graph
+
+DEFAULT_MAX_RETRIES = 1 << 20
+
+PROPOSALS = {"bi": _lib.PROPOSE_BI, "pairs": _lib.PROPOSE_PAIRS, "cutedge": _lib.PROPOSE_CUTEDGE}
+
+
+def population_bounds(total_pop: int, k: int, percent: float):
+    """Integer bounds equivalent to GerryChain's Bounds((1-p)*ideal, (1+p)*ideal)."""
+    ideal = total_pop / k
+    lo = (1 - percent) * ideal
+    hi = (1 + percent) * ideal
+    return int(math.ceil(lo)), int(math.floor(hi))
+
+
+def metropolis_table(base: float, maxdeg: int) -> np.ndarray:
+    """thr[d + maxdeg] = base ** (-d): cut_accept's bound for Δcut = d."""
+    b = float(base)
+    return np.array([b ** (-d) for d in range(-maxdeg, maxdeg + 1)], dtype=np.float64)
+
+
+def expected_wait_sum(stats, n_nodes: int, k: int) -> np.ndarray:
+    """Σ_t E[geom_wait_t] = (N^k - 1) * Σ 1/|B_t| - T (geom_wait, grid_chain_sec11.py:147-148)."""
+    M = float(n_nodes ** k - 1)
+    return M * stats["sum_invb"] - stats["yields"].astype(np.float64)
+
+
+class DeviceGraph:
+    """A CSR graph uploaded to one HIP device (fw_graph)."""
+
+    def __init__(self, graph: Graph, device: int = 0):
+        L = _lib.require_device()
+        self.graph = graph
+        self.device = device
+        h = _lib.ctypes.c_void_p()
+        rowptr = np.ascontiguousarray(graph.rowptr, np.int32)
+        col = np.ascontiguousarray(graph.col, np.int32)
+        pop = None if graph.pop is None else np.ascontiguousarray(graph.pop, np.int64)
+        check(L.fw_graph_create(ptr(rowptr), ptr(col), ptr(pop), graph.n, len(col), device,
+                                _lib.ctypes.byref(h)))
+        self._h = h
+        info = np.zeros(5, np.int64)
+        check(L.fw_graph_info(self._h, ptr(info)))
+        self.n, self.n_edges, self.maxdeg, self.grid_w, self.grid_h = (int(x) for x in info)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().fw_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Chains:
+    """n_chains independent flip walks resident on one device (fw_chains)."""
+
+    def __init__(self, dgraph: DeviceGraph, n_chains: int, k: int, init_labels,
+                 proposal: str | int = "pairs", pop_bounds=None, percent: float = 0.05,
+                 base: float | Sequence[float] = 1.0, seed: int = 0, chain_id0: int = 0):
+        L = _lib.require_device()
+        self.dgraph = dgraph
+        g = dgraph.graph
+        self.n_chains, self.k = int(n_chains), int(k)
+        self.mode = PROPOSALS[proposal] if isinstance(proposal, str) else int(proposal)
+        lab = np.ascontiguousarray(init_labels, np.int16)
+        per_chain = 1 if lab.ndim == 2 and lab.shape[0] == n_chains and n_chains > 1 else 0
+        if lab.ndim == 2 and not per_chain:
+            lab = np.ascontiguousarray(lab[0])
+        if pop_bounds is None:
+            pop_bounds = population_bounds(g.total_pop, k, percent)
+        self.pop_lo, self.pop_hi = int(pop_bounds[0]), int(pop_bounds[1])
+        D = dgraph.maxdeg
+        if np.ndim(base) == 0:
+            thr = metropolis_table(float(base), D)
+            thr_per = 0
+        else:
+            bases = np.asarray(base, np.float64)
+            if len(bases) != n_chains:
+                raise ValueError("per-chain bases need one base per chain")
+            thr = np.stack([metropolis_table(float(b), D) for b in bases])
+            thr_per = 1
+        self.thr = np.ascontiguousarray(thr)
+        self.seed, self.chain_id0 = int(seed), int(chain_id0)
+        h = _lib.ctypes.c_void_p()
+        check(L.fw_chains_create(dgraph.handle, self.n_chains, self.k, ptr(lab), per_chain,
+                                 self.mode, self.pop_lo, self.pop_hi, ptr(self.thr), thr_per,
+                                 self.seed & (2**64 - 1), self.chain_id0, _lib.ctypes.byref(h)))
+        self._h = h
+
+    # ------------------------------------------------------------- stepping
+    def run(self, steps: int, max_retries: int = DEFAULT_MAX_RETRIES) -> None:
+        check(_lib.load().fw_chains_run(self._h, int(steps), int(max_retries)))
+
+    def run_async(self, steps: int, max_retries: int = DEFAULT_MAX_RETRIES) -> None:
+        check(_lib.load().fw_chains_run_async(self._h, int(steps), int(max_retries)))
+
+    def sync(self) -> None:
+        check(_lib.load().fw_chains_sync(self._h))
+
+    def run_traced(self, steps: int, max_retries: int = DEFAULT_MAX_RETRIES) -> np.ndarray:
+        tr = np.empty((self.n_chains, int(steps)), np.int32)
+        check(_lib.load().fw_chains_run_traced(self._h, int(steps), int(max_retries), ptr(tr),
+                                               tr.nbytes))
+        return tr
+
+    def last_kernel_ms(self) -> float:
+        return float(_lib.load().fw_chains_last_kernel_ms(self._h))
+
+    def reset_observables(self) -> None:
+        check(_lib.load().fw_chains_reset_observables(self._h))
+
+    # ------------------------------------------------------------- reading
+    def _read(self, what, arr):
+        check(_lib.load().fw_chains_read(self._h, what, ptr(arr), arr.nbytes))
+        return arr
+
+    def labels(self) -> np.ndarray:
+        return self._read(_lib.READ_LABELS, np.empty((self.n_chains, self.dgraph.n), np.int16))
+
+    def stats(self) -> np.ndarray:
+        return self._read(_lib.READ_STATS, np.empty(self.n_chains, STATS_DTYPE))
+
+    def hist_cut(self) -> np.ndarray:
+        return self._read(_lib.READ_HIST_CUT, np.empty(self.dgraph.n_edges + 1, np.uint64))
+
+    def hist_b(self) -> np.ndarray:
+        return self._read(_lib.READ_HIST_B, np.empty(self.dgraph.n + 1, np.uint64))
+
+    def pops(self) -> np.ndarray:
+        return self._read(_lib.READ_POPS, np.empty((self.n_chains, self.k), np.int64))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().fw_chains_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def eval_flips(dgraph: DeviceGraph, labels, k: int, v, target, pop_bounds):
+    """Batched per-flip verdicts on one state (fw_eval_flips)."""
+    L = _lib.require_device()
+    lab = np.ascontiguousarray(labels, np.int16)
+    v = np.ascontiguousarray(v, np.int32)
+    t = np.ascontiguousarray(target, np.int16)
+    m = len(v)
+    dcut = np.zeros(m, np.int32)
+    contig = np.zeros(m, np.uint8)
+    pop_ok = np.zeros(m, np.uint8)
+    db = np.zeros(m, np.int32)
+    check(L.fw_eval_flips(dgraph.handle, ptr(lab), int(k), ptr(v), ptr(t), m, int(pop_bounds[0]),
+                          int(pop_bounds[1]), ptr(dcut), ptr(contig), ptr(pop_ok), ptr(db)))
+    return dcut, contig, pop_ok, db
+
+
+@dataclass
+class RunResult:
+    labels: np.ndarray      # [n_chains, n] final plans
+    stats: np.ndarray       # [n_chains] STATS_DTYPE
+    hist_cut: np.ndarray    # yields per |cut edges|
+    hist_b: np.ndarray      # yields per |B|
+    pops: np.ndarray        # [n_chains, k]
+    kernel_ms: float
+
+    def expected_wait_sums(self, n_nodes: int, k: int) -> np.ndarray:
+        return expected_wait_sum(self.stats, n_nodes, k)
+
+
+def run_chains(graph: Graph, init_labels, k: int, n_chains: int, steps: int,
+               proposal: str | int = "pairs", percent: float = 0.05, base=1.0, seed: int = 0,
+               chain_id0: int = 0, device: int = 0, pop_bounds=None,
+               max_retries: int = DEFAULT_MAX_RETRIES, total_steps: Optional[int] = None
+               ) -> RunResult:
+    """Run ``n_chains`` chains for ``steps`` counted steps each and read everything back.
+
+    ``total_steps`` (GerryChain's meaning: yields including the initial state) may be
+    given instead of ``steps``; then steps = total_steps - 1.
+    """
+    if total_steps is not None:
+        steps = int(total_steps) - 1
+    dg = DeviceGraph(graph, device)
+    ch = Chains(dg, n_chains, k, init_labels, proposal=proposal, pop_bounds=pop_bounds,
+                percent=percent, base=base, seed=seed, chain_id0=chain_id0)
+    ch.run(steps, max_retries)
+    res = RunResult(ch.labels(), ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(),
+                    ch.last_kernel_ms())
+    ch.close()
+    dg.close()
+    return res

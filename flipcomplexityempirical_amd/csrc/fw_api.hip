@@ -1,0 +1,630 @@
+// fw_api.hip — host implementation of the C-ABI in include/flipwalk.h.
+//
+// Owns device memory behind fw_graph / fw_chains handles, validates inputs the
+// way GerryChain does (initial-state check -> FW_ESTATE, like MarkovChain's
+// ValueError), packs labels into the kernels' LB-bit layout and launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fw_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(FW_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));             \
+  } while (0)
+
+int round16(int64_t x) { return (int)((x + 15) / 16 * 16); }
+
+// Same rule as flipcomplexityempirical_amd.graph.detect_grid.
+int detect_grid(const std::vector<int32_t>& rp, const std::vector<int32_t>& col, int n) {
+  if (n < 4) return 0;
+  if (rp[1] - rp[0] != 2 || col[0] != 1) return 0;
+  const int w = col[1];
+  if (w < 2 || n % w || n / w < 2) return 0;
+  const int h = n / w;
+  int e = 0;
+  for (int i = 0; i < h; ++i)
+    for (int j = 0; j < w; ++j) {
+      const int x = i * w + j;
+      int nb[4], d = 0;
+      if (i > 0) nb[d++] = x - w;
+      if (j > 0) nb[d++] = x - 1;
+      if (j < w - 1) nb[d++] = x + 1;
+      if (i < h - 1) nb[d++] = x + w;
+      if (rp[x] != e || rp[x + 1] - rp[x] != d) return 0;
+      for (int t = 0; t < d; ++t)
+        if (col[e + t] != nb[t]) return 0;
+      e += d;
+    }
+  return w;
+}
+
+}  // namespace
+
+struct fw_graph {
+  int device = 0;
+  int32_t n = 0, nnz = 0, maxdeg = 0, gw = 0, gh = 0;
+  std::vector<int32_t> rowptr, col;
+  std::vector<int64_t> pop;  // empty: unit populations
+  int32_t* d_rowptr = nullptr;
+  int32_t* d_col = nullptr;
+  int64_t* d_pop = nullptr;
+  int64_t popof(int x) const { return pop.empty() ? 1 : pop[x]; }
+  FwGraphDev dev() const {
+    FwGraphDev g;
+    g.rowptr = d_rowptr;
+    g.col = d_col;
+    g.pop = d_pop;
+    g.n = n;
+    g.nedges = nnz / 2;
+    g.maxdeg = maxdeg;
+    g.gw = gw;
+    g.gh = gh;
+    return g;
+  }
+};
+
+struct fw_chains {
+  fw_graph* g = nullptr;
+  int32_t n_chains = 0, k = 0, mode = 0, lb = 4, grid = 1, D = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  FwRunParams p{};
+  uint8_t* d_labels = nullptr;
+  fw_chain_stats* d_stats = nullptr;
+  int64_t* d_pops = nullptr;
+  double* d_thr = nullptr;
+  unsigned long long* d_hist_cut = nullptr;
+  unsigned long long* d_hist_b = nullptr;
+  uint32_t* d_spill = nullptr;
+  int32_t* d_next = nullptr;
+};
+
+namespace {
+
+// Label bits per node for a (k, maxdeg): the search marks visited nodes with codes
+// k..k+deg-1 and v with the all-ones value, so k + maxdeg must stay below it.
+int pick_lb(int k, int maxdeg) {
+  if (k + maxdeg <= 15 && maxdeg <= 15) return 4;
+  if (k + maxdeg <= 255) return 8;
+  return 0;
+}
+
+void pack_labels(const int16_t* lab, int n, int lb, uint8_t* out, int bytes) {
+  std::memset(out, 0, (size_t)bytes);
+  if (lb == 8) {
+    for (int x = 0; x < n; ++x) out[x] = (uint8_t)lab[x];
+  } else {
+    for (int x = 0; x < n; ++x) out[x >> 1] |= (uint8_t)((lab[x] & 15) << ((x & 1) * 4));
+  }
+}
+
+void unpack_labels(const uint8_t* in, int n, int lb, int16_t* lab) {
+  if (lb == 8) {
+    for (int x = 0; x < n; ++x) lab[x] = in[x];
+  } else {
+    for (int x = 0; x < n; ++x) lab[x] = (in[x >> 1] >> ((x & 1) * 4)) & 15;
+  }
+}
+
+// MarkovChain's initial-state validity: every district non-empty, connected and
+// inside the population bounds.  Fills pops[k].
+bool plan_valid(const fw_graph* g, const int16_t* lab, int k, int64_t lo, int64_t hi,
+                int64_t* pops, std::string* why) {
+  const int n = g->n;
+  std::vector<int> first(k, -1);
+  for (int d = 0; d < k; ++d) pops[d] = 0;
+  for (int x = 0; x < n; ++x) {
+    if (lab[x] < 0 || lab[x] >= k) {
+      *why = "label out of range at node " + std::to_string(x);
+      return false;
+    }
+    pops[lab[x]] += g->popof(x);
+    if (first[lab[x]] < 0) first[lab[x]] = x;
+  }
+  std::vector<uint8_t> seen(n, 0);
+  std::vector<int> q(n);
+  for (int d = 0; d < k; ++d) {
+    if (first[d] < 0) {
+      *why = "district " + std::to_string(d) + " is empty";
+      return false;
+    }
+    if (pops[d] < lo || pops[d] > hi) {
+      *why = "district " + std::to_string(d) + " population " + std::to_string(pops[d]) +
+             " outside [" + std::to_string(lo) + ", " + std::to_string(hi) + "]";
+      return false;
+    }
+    int h = 0, t = 0;
+    q[t++] = first[d];
+    seen[first[d]] = 1;
+    while (h < t) {
+      int x = q[h++];
+      for (int e = g->rowptr[x]; e < g->rowptr[x + 1]; ++e) {
+        int y = g->col[e];
+        if (!seen[y] && lab[y] == d) {
+          seen[y] = 1;
+          q[t++] = y;
+        }
+      }
+    }
+  }
+  for (int x = 0; x < n; ++x)
+    if (!seen[x]) {
+      *why = "district " + std::to_string(lab[x]) + " is not contiguous (node " +
+             std::to_string(x) + ")";
+      return false;
+    }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fw_last_error(void) { return g_err.c_str(); }
+
+int32_t fw_version(void) { return 0x000100; }
+
+int32_t fw_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* pop, int32_t n,
+                    int32_t nnz, int device, fw_graph** out) {
+  if (!out || !rowptr || (nnz > 0 && !col) || n <= 0 || nnz < 0)
+    return fail(FW_EINVAL, "fw_graph_create: bad arguments");
+  *out = nullptr;
+  if (rowptr[0] != 0 || rowptr[n] != nnz) return fail(FW_EINVAL, "rowptr[0]/rowptr[n] mismatch");
+  auto g = new fw_graph();
+  g->device = device;
+  g->n = n;
+  g->nnz = nnz;
+  g->rowptr.assign(rowptr, rowptr + n + 1);
+  g->col.assign(col, col + nnz);
+  bool unit = true;
+  if (pop) {
+    for (int x = 0; x < n; ++x) unit &= pop[x] == 1;
+    if (!unit) g->pop.assign(pop, pop + n);
+  }
+  for (int x = 0; x < n; ++x) {
+    const int b = rowptr[x], e = rowptr[x + 1];
+    if (e < b) {
+      delete g;
+      return fail(FW_EINVAL, "rowptr not monotone at %d", x);
+    }
+    g->maxdeg = std::max(g->maxdeg, e - b);
+    for (int t = b; t < e; ++t) {
+      const int y = col[t];
+      if (y < 0 || y >= n || y == x || (t > b && col[t - 1] >= y)) {
+        delete g;
+        return fail(FW_EINVAL, "row %d: neighbours must be ascending, in range, no self loop", x);
+      }
+      // symmetry: x must appear in y's (sorted) row
+      if (!std::binary_search(col + rowptr[y], col + rowptr[y + 1], x)) {
+        delete g;
+        return fail(FW_EINVAL, "adjacency not symmetric: %d->%d", x, y);
+      }
+    }
+  }
+  g->gw = detect_grid(g->rowptr, g->col, n);
+  g->gh = g->gw ? n / g->gw : 0;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete g;
+    return fail(FW_EHIP, "hipSetDevice(%d) failed", device);
+  }
+  hipError_t e1 = hipMalloc(&g->d_rowptr, sizeof(int32_t) * (n + 1));
+  hipError_t e2 = hipMalloc(&g->d_col, sizeof(int32_t) * std::max(nnz, 1));
+  hipError_t e3 = g->pop.empty() ? hipSuccess : hipMalloc(&g->d_pop, sizeof(int64_t) * n);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+    fw_graph_destroy(g);
+    return fail(FW_EHIP, "hipMalloc failed for graph");
+  }
+  bool up = hipMemcpy(g->d_rowptr, rowptr, sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice) ==
+            hipSuccess;
+  if (nnz) up &= hipMemcpy(g->d_col, col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice) == hipSuccess;
+  if (g->d_pop)
+    up &= hipMemcpy(g->d_pop, g->pop.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice) ==
+          hipSuccess;
+  if (!up || hipDeviceSynchronize() != hipSuccess) {
+    fw_graph_destroy(g);
+    return fail(FW_EHIP, "graph upload failed");
+  }
+  *out = g;
+  return FW_OK;
+}
+
+void fw_graph_destroy(fw_graph* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  if (g->d_rowptr) (void)hipFree(g->d_rowptr);
+  if (g->d_col) (void)hipFree(g->d_col);
+  if (g->d_pop) (void)hipFree(g->d_pop);
+  delete g;
+}
+
+int fw_graph_info(const fw_graph* g, int64_t info[5]) {
+  if (!g || !info) return fail(FW_EINVAL, "fw_graph_info: null");
+  info[0] = g->n;
+  info[1] = g->nnz / 2;
+  info[2] = g->maxdeg;
+  info[3] = g->gw;
+  info[4] = g->gh;
+  return FW_OK;
+}
+
+void fw_chains_destroy(fw_chains* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->g->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_hist_cut, c->d_hist_b,
+                  c->d_spill, c->d_next};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* init_labels,
+                     int32_t init_per_chain, int32_t proposal_mode, int64_t pop_lo, int64_t pop_hi,
+                     const double* thr, int32_t thr_per_chain, uint64_t seed, int64_t chain_id0,
+                     fw_chains** out) {
+  if (!out || !g || !init_labels || !thr || n_chains <= 0)
+    return fail(FW_EINVAL, "fw_chains_create: bad arguments");
+  *out = nullptr;
+  if (k < 2 || k > FW_MAX_K) return fail(FW_EUNSUPPORTED, "k=%d outside [2, %d]", k, FW_MAX_K);
+  if (proposal_mode < FW_PROPOSE_BI || proposal_mode > FW_PROPOSE_CUTEDGE)
+    return fail(FW_EINVAL, "unknown proposal mode %d", proposal_mode);
+  if (proposal_mode == FW_PROPOSE_BI && k != 2)
+    return fail(FW_EINVAL, "slow_reversible_propose_bi needs k == 2 (got %d)", k);
+  if (g->maxdeg > FW_MAX_DEG)
+    return fail(FW_EUNSUPPORTED, "max degree %d > %d", g->maxdeg, FW_MAX_DEG);
+  const int lb = pick_lb(k, g->maxdeg);
+  if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
+  const int n = g->n, D = g->maxdeg;
+  const int G = (n + 63) / 64;
+
+  auto c = new fw_chains();
+  c->g = g;
+  c->n_chains = n_chains;
+  c->k = k;
+  c->mode = proposal_mode == FW_PROPOSE_BI ? FW_PROPOSE_PAIRS : proposal_mode;
+  c->lb = lb;
+  c->D = D;
+
+  // ---- LDS layout
+  FwRunParams& p = c->p;
+  p.qcap = 512;
+  p.lab_bytes = round16(((int64_t)n * lb + 7) / 8);
+  p.off_w = p.lab_bytes;
+  p.off_gsum = p.off_w + round16((int64_t)G * 64 * lb / 8);
+  p.off_pops = p.off_gsum + round16((int64_t)G * 4);
+  p.off_list = p.off_pops + round16((int64_t)k * 8);
+  p.lds_bytes = p.off_list + p.qcap * 4;
+  if (p.lds_bytes > 160 * 1024 - 64) {
+    delete c;
+    return fail(FW_EUNSUPPORTED, "graph too large for LDS-resident chains (%d B)", p.lds_bytes);
+  }
+
+  // ---- initial-state validation and populations
+  const int ninit = init_per_chain ? n_chains : 1;
+  std::vector<int64_t> pops0((size_t)ninit * k);
+  for (int i = 0; i < ninit; ++i) {
+    std::string why;
+    if (!plan_valid(g, init_labels + (size_t)i * n, k, pop_lo, pop_hi, pops0.data() + (size_t)i * k,
+                    &why)) {
+      delete c;
+      return fail(FW_ESTATE, "initial plan%s invalid: %s",
+                  init_per_chain ? (" " + std::to_string(i)).c_str() : "", why.c_str());
+    }
+  }
+  const int lab_stride = p.lab_bytes;
+  std::vector<uint8_t> packed((size_t)n_chains * lab_stride);
+  std::vector<int64_t> pops((size_t)n_chains * k);
+  {
+    std::vector<uint8_t> one(lab_stride);
+    for (int i = 0; i < ninit; ++i) {
+      pack_labels(init_labels + (size_t)i * n, n, lb, packed.data() + (size_t)i * lab_stride,
+                  lab_stride);
+    }
+    for (int i = ninit; i < n_chains; ++i)
+      std::memcpy(packed.data() + (size_t)i * lab_stride, packed.data(), lab_stride);
+    for (int i = 0; i < n_chains; ++i)
+      std::memcpy(pops.data() + (size_t)i * k, pops0.data() + (size_t)(init_per_chain ? i : 0) * k,
+                  sizeof(int64_t) * k);
+  }
+
+  if (hipSetDevice(g->device) != hipSuccess) {
+    delete c;
+    return fail(FW_EHIP, "hipSetDevice failed");
+  }
+  p.g = g->dev();
+  p.n_chains = n_chains;
+  p.k = k;
+  p.mode = c->mode;
+  p.G = G;
+  p.pop_lo = pop_lo;
+  p.pop_hi = pop_hi;
+  p.seed = seed;
+  p.chain_id0 = chain_id0;
+  p.lab_stride = lab_stride;
+  p.thr_stride = thr_per_chain ? 2 * D + 1 : 0;
+  if (fw_run_grid_size(p, lb, g->device, &c->grid) != 0) {
+    delete c;
+    return fail(FW_EHIP, "occupancy query failed (LDS %d B)", p.lds_bytes);
+  }
+  const size_t nthr = (size_t)(thr_per_chain ? n_chains : 1) * (2 * D + 1);
+  bool ok = hipMalloc(&c->d_labels, packed.size()) == hipSuccess &&
+            hipMalloc(&c->d_stats, sizeof(fw_chain_stats) * n_chains) == hipSuccess &&
+            hipMalloc(&c->d_pops, sizeof(int64_t) * pops.size()) == hipSuccess &&
+            hipMalloc(&c->d_thr, sizeof(double) * nthr) == hipSuccess &&
+            hipMalloc(&c->d_hist_cut, sizeof(unsigned long long) * (g->nnz / 2 + 1 + FW_HIST_PAD)) ==
+                hipSuccess &&
+            hipMalloc(&c->d_hist_b, sizeof(unsigned long long) * (n + 1 + FW_HIST_PAD)) ==
+                hipSuccess &&
+            hipMalloc(&c->d_spill, sizeof(uint32_t) * (size_t)c->grid * n) == hipSuccess &&
+            hipMalloc(&c->d_next, sizeof(int32_t)) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess;
+  if (!ok) {
+    fw_chains_destroy(c);
+    return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
+  }
+  ok = hipMemcpy(c->d_labels, packed.data(), packed.size(), hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->d_pops, pops.data(), sizeof(int64_t) * pops.size(), hipMemcpyHostToDevice) ==
+           hipSuccess &&
+       hipMemcpy(c->d_thr, thr, sizeof(double) * nthr, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemset(c->d_stats, 0, sizeof(fw_chain_stats) * n_chains) == hipSuccess &&
+       hipMemset(c->d_hist_cut, 0, sizeof(unsigned long long) * (g->nnz / 2 + 1 + FW_HIST_PAD)) ==
+           hipSuccess &&
+       hipMemset(c->d_hist_b, 0, sizeof(unsigned long long) * (n + 1 + FW_HIST_PAD)) == hipSuccess;
+  if (!ok || hipDeviceSynchronize() != hipSuccess) {
+    fw_chains_destroy(c);
+    return fail(FW_EHIP, "chain upload failed");
+  }
+  p.labels = c->d_labels;
+  p.stats = c->d_stats;
+  p.pops = c->d_pops;
+  p.thr = c->d_thr;
+  p.hist_cut = c->d_hist_cut;
+  p.hist_b = c->d_hist_b;
+  p.spill = c->d_spill;
+  p.next_chain = c->d_next;
+  *out = c;
+  return FW_OK;
+}
+
+int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
+  if (!c || steps < 0 || max_retries <= 0) return fail(FW_EINVAL, "fw_chains_run: bad arguments");
+  HIPCHK(hipSetDevice(c->g->device));
+  if (steps == 0) return FW_OK;
+  c->p.steps = steps;
+  c->p.max_retries = max_retries;
+  HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if (fw_launch_run(c->p, c->lb, c->grid, c->stream) != 0)
+    return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  return FW_OK;
+}
+
+int fw_chains_sync(fw_chains* c) {
+  if (!c) return fail(FW_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return FW_OK;
+}
+
+int fw_chains_run(fw_chains* c, int64_t steps, int32_t max_retries) {
+  int rc = fw_chains_run_async(c, steps, max_retries);
+  if (rc) return rc;
+  return fw_chains_sync(c);
+}
+
+int fw_chains_run_traced(fw_chains* c, int64_t steps, int32_t max_retries, int32_t* host_trace,
+                         size_t bytes) {
+  if (!c || !host_trace || steps <= 0) return fail(FW_EINVAL, "fw_chains_run_traced: bad arguments");
+  const size_t need = sizeof(int32_t) * (size_t)c->n_chains * (size_t)steps;
+  if (bytes < need) return fail(FW_EINVAL, "trace needs %zu bytes", need);
+  HIPCHK(hipSetDevice(c->g->device));
+  int32_t* d_trace = nullptr;
+  HIPCHK(hipMalloc(&d_trace, need));
+  int rc = FW_OK;
+  if (hipMemsetAsync(d_trace, 0xFE, need, c->stream) != hipSuccess) {
+    rc = fail(FW_EHIP, "trace memset failed");
+  } else {
+    c->p.trace = d_trace;
+    rc = fw_chains_run(c, steps, max_retries);
+    c->p.trace = nullptr;
+    if (rc == FW_OK && hipMemcpy(host_trace, d_trace, need, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(FW_EHIP, "trace download failed");
+  }
+  (void)hipFree(d_trace);
+  return rc;
+}
+
+double fw_chains_last_kernel_ms(const fw_chains* c) {
+  if (!c || !c->timed) return -1.0;
+  float ms = -1.f;
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0;
+  return ms;
+}
+
+int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes) {
+  if (!c || !host_dst) return fail(FW_EINVAL, "fw_chains_read: null");
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int n = c->g->n;
+  size_t need = 0;
+  switch (what) {
+    case FW_READ_LABELS: {
+      need = sizeof(int16_t) * (size_t)c->n_chains * n;
+      if (bytes < need) return fail(FW_EINVAL, "labels need %zu bytes", need);
+      std::vector<uint8_t> packed((size_t)c->n_chains * c->p.lab_stride);
+      HIPCHK(hipMemcpy(packed.data(), c->d_labels, packed.size(), hipMemcpyDeviceToHost));
+      for (int i = 0; i < c->n_chains; ++i)
+        unpack_labels(packed.data() + (size_t)i * c->p.lab_stride, n, c->lb,
+                      static_cast<int16_t*>(host_dst) + (size_t)i * n);
+      return FW_OK;
+    }
+    case FW_READ_STATS:
+      need = sizeof(fw_chain_stats) * c->n_chains;
+      if (bytes < need) return fail(FW_EINVAL, "stats need %zu bytes", need);
+      HIPCHK(hipMemcpy(host_dst, c->d_stats, need, hipMemcpyDeviceToHost));
+      return FW_OK;
+    case FW_READ_HIST_CUT:
+      need = sizeof(uint64_t) * (c->g->nnz / 2 + 1);
+      if (bytes < need) return fail(FW_EINVAL, "hist_cut needs %zu bytes", need);
+      HIPCHK(hipMemcpy(host_dst, c->d_hist_cut, need, hipMemcpyDeviceToHost));
+      return FW_OK;
+    case FW_READ_HIST_B:
+      need = sizeof(uint64_t) * (n + 1);
+      if (bytes < need) return fail(FW_EINVAL, "hist_b needs %zu bytes", need);
+      HIPCHK(hipMemcpy(host_dst, c->d_hist_b, need, hipMemcpyDeviceToHost));
+      return FW_OK;
+    case FW_READ_POPS:
+      need = sizeof(int64_t) * (size_t)c->n_chains * c->k;
+      if (bytes < need) return fail(FW_EINVAL, "pops need %zu bytes", need);
+      HIPCHK(hipMemcpy(host_dst, c->d_pops, need, hipMemcpyDeviceToHost));
+      return FW_OK;
+    default:
+      return fail(FW_EINVAL, "unknown read kind %d", what);
+  }
+}
+
+int fw_chains_reset_observables(fw_chains* c) {
+  if (!c) return fail(FW_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  std::vector<fw_chain_stats> st(c->n_chains);
+  HIPCHK(hipMemcpy(st.data(), c->d_stats, sizeof(fw_chain_stats) * st.size(),
+                   hipMemcpyDeviceToHost));
+  for (auto& s : st) {
+    s.yields = 0;
+    s.sum_cut = 0;
+    s.sum_bnodes = 0;
+    s.sum_invb = 0.0;
+  }
+  HIPCHK(hipMemcpy(c->d_stats, st.data(), sizeof(fw_chain_stats) * st.size(),
+                   hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(c->d_hist_cut, 0,
+                   sizeof(unsigned long long) * (c->g->nnz / 2 + 1 + FW_HIST_PAD)));
+  HIPCHK(hipMemset(c->d_hist_b, 0, sizeof(unsigned long long) * (c->g->n + 1 + FW_HIST_PAD)));
+  return FW_OK;
+}
+
+int fw_eval_flips(fw_graph* g, const int16_t* labels, int32_t k, const int32_t* v,
+                  const int16_t* target, int32_t m, int64_t pop_lo, int64_t pop_hi, int32_t* dcut,
+                  uint8_t* contig, uint8_t* pop_ok, int32_t* dboundary) {
+  if (!g || !labels || (m > 0 && (!v || !target || !dcut || !contig || !pop_ok || !dboundary)) ||
+      m < 0)
+    return fail(FW_EINVAL, "fw_eval_flips: bad arguments");
+  if (m == 0) return FW_OK;
+  if (k < 2 || k > FW_MAX_K) return fail(FW_EUNSUPPORTED, "k=%d outside [2, %d]", k, FW_MAX_K);
+  if (g->maxdeg > FW_MAX_DEG) return fail(FW_EUNSUPPORTED, "max degree %d", g->maxdeg);
+  const int lb = pick_lb(k, g->maxdeg);
+  if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg too large");
+  const int n = g->n;
+  std::vector<int64_t> pops(k, 0);
+  for (int x = 0; x < n; ++x) {
+    if (labels[x] < 0 || labels[x] >= k) return fail(FW_EINVAL, "label out of range at %d", x);
+    pops[labels[x]] += g->popof(x);
+  }
+  for (int i = 0; i < m; ++i) {
+    if (v[i] < 0 || v[i] >= n || target[i] < 0 || target[i] >= k || target[i] == labels[v[i]])
+      return fail(FW_EINVAL, "flip %d (v=%d, target=%d) is not a relabelling", i, v[i], target[i]);
+  }
+  FwEvalParams p{};
+  p.qcap = 512;
+  p.lab_bytes = round16(((int64_t)n * lb + 7) / 8);
+  p.off_list = p.lab_bytes;
+  p.lds_bytes = p.off_list + p.qcap * 4;
+  if (p.lds_bytes > 160 * 1024 - 64) return fail(FW_EUNSUPPORTED, "graph too large for LDS");
+  std::vector<uint8_t> packed(p.lab_bytes);
+  pack_labels(labels, n, lb, packed.data(), p.lab_bytes);
+  HIPCHK(hipSetDevice(g->device));
+  const int grid = std::min(m, 2048);
+  uint8_t* d_lab = nullptr;
+  int64_t* d_pops = nullptr;
+  int32_t *d_v = nullptr, *d_dcut = nullptr, *d_db = nullptr;
+  int16_t* d_t = nullptr;
+  uint8_t *d_contig = nullptr, *d_pok = nullptr;
+  uint32_t* d_spill = nullptr;
+  bool ok = hipMalloc(&d_lab, p.lab_bytes) == hipSuccess &&
+            hipMalloc(&d_pops, sizeof(int64_t) * k) == hipSuccess &&
+            hipMalloc(&d_v, sizeof(int32_t) * m) == hipSuccess &&
+            hipMalloc(&d_t, sizeof(int16_t) * m) == hipSuccess &&
+            hipMalloc(&d_dcut, sizeof(int32_t) * m) == hipSuccess &&
+            hipMalloc(&d_db, sizeof(int32_t) * m) == hipSuccess &&
+            hipMalloc(&d_contig, m) == hipSuccess && hipMalloc(&d_pok, m) == hipSuccess &&
+            hipMalloc(&d_spill, sizeof(uint32_t) * (size_t)grid * n) == hipSuccess;
+  int rc = FW_OK;
+  if (!ok) {
+    rc = fail(FW_ENOMEM, "device allocation failed in fw_eval_flips");
+  } else {
+    ok = hipMemcpy(d_lab, packed.data(), p.lab_bytes, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_pops, pops.data(), sizeof(int64_t) * k, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_v, v, sizeof(int32_t) * m, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_t, target, sizeof(int16_t) * m, hipMemcpyHostToDevice) == hipSuccess;
+    p.g = g->dev();
+    p.labels = d_lab;
+    p.pops = d_pops;
+    p.k = k;
+    p.m = m;
+    p.v = d_v;
+    p.target = d_t;
+    p.pop_lo = pop_lo;
+    p.pop_hi = pop_hi;
+    p.dcut = d_dcut;
+    p.contig = d_contig;
+    p.pop_ok = d_pok;
+    p.dboundary = d_db;
+    p.spill = d_spill;
+    if (!ok) {
+      rc = fail(FW_EHIP, "upload failed in fw_eval_flips");
+    } else if (fw_launch_eval(p, lb, grid, nullptr) != 0) {
+      rc = fail(FW_EHIP, "eval launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else if (hipDeviceSynchronize() != hipSuccess) {
+      rc = fail(FW_EHIP, "eval kernel failed: %s", hipGetErrorString(hipGetLastError()));
+    } else {
+      ok = hipMemcpy(dcut, d_dcut, sizeof(int32_t) * m, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(dboundary, d_db, sizeof(int32_t) * m, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(contig, d_contig, m, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(pop_ok, d_pok, m, hipMemcpyDeviceToHost) == hipSuccess;
+      if (!ok) rc = fail(FW_EHIP, "download failed in fw_eval_flips");
+    }
+  }
+  void* bufs[] = {d_lab, d_pops, d_v, d_t, d_dcut, d_db, d_contig, d_pok, d_spill};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  return rc;
+}
+
+}  // extern "C"

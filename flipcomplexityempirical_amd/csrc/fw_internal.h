@@ -1,0 +1,69 @@
+// fw_internal.h — structs shared by the host API (fw_api.hip) and the kernels
+// (fw_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/flipwalk.h"
+
+// Kernel-variant limits (checked on the host before any launch).
+#define FW_MAX_DEG 63   // lanes 1..deg of one wave hold v's neighbours during commit
+#define FW_MAX_K 64     // foreign-label sets are 64-bit masks
+#define FW_HIST_PAD 64  // histogram window slack past the last bin
+
+struct FwGraphDev {
+  const int32_t* rowptr;  // [n+1]
+  const int32_t* col;     // [nnz]
+  const int64_t* pop;     // [n] or nullptr (unit populations)
+  int32_t n, nedges, maxdeg;
+  int32_t gw, gh;         // grid width/height (gw == 0: general CSR)
+};
+
+struct FwRunParams {
+  FwGraphDev g;
+  uint8_t* labels;             // packed LB-bit labels, chain c at labels + c*lab_stride
+  int64_t lab_stride;          // bytes per chain (multiple of 16)
+  fw_chain_stats* stats;       // [n_chains]
+  int64_t* pops;               // [n_chains][k]
+  const double* thr;           // [n_chains or 1][2*maxdeg+1]
+  int32_t thr_stride;          // 0 (shared table) or 2*maxdeg+1
+  unsigned long long* hist_cut;  // [nedges+1+FW_HIST_PAD]
+  unsigned long long* hist_b;    // [n+1+FW_HIST_PAD]
+  uint32_t* spill;             // [grid][n] search-list spill
+  int32_t* next_chain;         // dynamic chain counter (zeroed before launch)
+  int32_t* trace;              // optional [n_chains][steps]: v*64+target if accepted, -1 if not
+  int32_t n_chains, k, mode, G;  // G = ceil(n/64) weight groups
+  int64_t pop_lo, pop_hi;
+  uint64_t seed;
+  int64_t chain_id0;
+  int64_t steps;
+  int32_t max_retries;
+  int32_t qcap;                // search-list entries held in LDS
+  // LDS layout (bytes from the dynamic shared base)
+  int32_t lab_bytes;           // packed label bytes (multiple of 16)
+  int32_t off_w, off_gsum, off_pops, off_list, lds_bytes;
+};
+
+struct FwEvalParams {
+  FwGraphDev g;
+  const uint8_t* labels;  // packed LB-bit labels of the one state
+  int32_t lab_bytes;
+  const int64_t* pops;    // [k] populations of the state
+  int32_t k, m;
+  const int32_t* v;
+  const int16_t* target;
+  int64_t pop_lo, pop_hi;
+  int32_t* dcut;
+  uint8_t* contig;
+  uint8_t* pop_ok;
+  int32_t* dboundary;
+  uint32_t* spill;        // [grid][n]
+  int32_t qcap;
+  int32_t off_list, lds_bytes;
+};
+
+// Host-side launchers implemented in fw_kernels.hip.
+int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
+int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
+int fw_run_grid_size(const FwRunParams& p, int lb, int device, int* grid);

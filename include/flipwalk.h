@@ -151,6 +151,14 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries);
 int fw_chains_sync(fw_chains* c);
 double fw_chains_last_kernel_ms(const fw_chains* c);
 
+/* fw_chains_run plus a per-step trace: host_trace [n_chains][steps] receives, for
+ * each counted step, v*64 + target when the flip was accepted, -1 when the
+ * Metropolis draw kept the old state, and a value < -1 for steps a stuck chain
+ * never took.  Used by the façade's GerryChain-style iterator to rebuild every
+ * yielded Partition on the host. */
+int fw_chains_run_traced(fw_chains* c, int64_t steps, int32_t max_retries, int32_t* host_trace,
+                         size_t bytes);
+
 /* Copy a state array back to the host (see FW_READ_*). */
 int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes);
 

@@ -415,7 +415,7 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
   c.hist_b = hist_b;
   derive(&c);
   const int32_t D = c.g.maxdeg;
-  if (c.st.yields == 0) yield_obs(&c);
+  if (c.st.yields == 0 && c.st.attempts == 0) yield_obs(&c);
   for (int64_t s = 0; s < steps && !c.st.stuck; ++s) {
     int32_t retries = 0;
     int32_t v = -1, dcut = 0;

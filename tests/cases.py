@@ -1,0 +1,74 @@
+"""Shared test configurations (graphs, seed plans, chain parameters).
+
+Graphs follow the reference's constructions: the plain grid (nx.grid_graph,
+grid_chain_sec11.py:191), the sec11 grid with corner diagonals and corners removed
+(:191-260), and the Kansas dual graphs (State_Data/*.json, All_States_Chain.py:208,221)
+from the committed CSR fixtures in tests/golden (the reference tree does not travel
+to the GPU box).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+from flipcomplexityempirical_amd.graph import (Graph, block_seed, grid_graph, sec11_graph,
+                                               sec11_seed, stripe_seed)
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MU = 2.63815853
+
+
+def kansas(name: str) -> Graph:
+    """Kansas dual graph from the committed CSR fixture (TOTPOP populations)."""
+    d = np.load(os.path.join(GOLDEN, f"kansas_{name}.npz"), allow_pickle=False)
+    g = Graph(rowptr=d["rowptr"], col=d["col"], pop=d["pop"], nodes=list(range(len(d["pop"]))))
+    return g
+
+
+def kansas_seed(name: str, k: int) -> np.ndarray:
+    d = np.load(os.path.join(GOLDEN, f"kansas_{name}.npz"), allow_pickle=False)
+    return d[f"seed_k{k}"].astype(np.int16)
+
+
+@dataclass
+class Case:
+    name: str
+    graph: Graph
+    init: np.ndarray
+    k: int
+    mode: int
+    percent: float
+    base: float
+
+    @property
+    def bounds(self):
+        return population_bounds(self.graph.total_pop, self.k, self.percent)
+
+    @property
+    def thr(self):
+        return metropolis_table(self.base, self.graph.maxdeg)
+
+
+def cases(include_kansas: bool = True):
+    out = [
+        Case("grid10_k2_bi", grid_graph(10, 10), stripe_seed(10, 10), 2, 0, 0.10, MU),
+        Case("grid12_k4_pairs", grid_graph(12, 12), block_seed(12, 12, 2, 2), 4, 1, 0.10, 0.5),
+        Case("grid12_k4_cut", grid_graph(12, 12), block_seed(12, 12, 2, 2), 4, 2, 0.10, 1.5),
+        Case("grid20_k4_mu", grid_graph(20, 20), block_seed(20, 20, 2, 2), 4, 1, 0.05, MU),
+        Case("grid16x24_k8", grid_graph(16, 24), block_seed(16, 24, 2, 4), 8, 1, 0.10, 1.0),
+    ]
+    g11 = sec11_graph()
+    out.append(Case("sec11_a2_k2", g11, sec11_seed(g11, 2), 2, 0, 0.05, 0.1))
+    out.append(Case("sec11_a0_k2_mu", g11, sec11_seed(g11, 0), 2, 0, 0.10, MU))
+    if include_kansas:
+        out.append(Case("county_k2", kansas("County20"), kansas_seed("County20", 2), 2, 0, 0.10,
+                        1.0))
+        out.append(Case("tract_k4", kansas("Tract20"), kansas_seed("Tract20", 4), 4, 1, 0.20,
+                        0.8))
+        out.append(Case("tract_k2_cut", kansas("Tract20"), kansas_seed("Tract20", 2), 2, 2, 0.20,
+                        MU))
+    return out

@@ -1,0 +1,122 @@
+"""GPU parity: the HIP path through the C-ABI against the CPU oracle, bit for bit.
+
+Every chain's final plan, every counter, the fp64 sum of 1/|B| (bitwise), the district
+populations and the yield histograms must equal oracle/flipchain_oracle.c run on the
+same (seed, global chain id).  The oracle's per-flip verdicts are themselves pinned to
+networkx ground truth (tests/golden/flips_golden.npz, tests/test_oracle.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from cases import GOLDEN, cases
+from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, eval_flips
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = cases()
+IDS = [c.name for c in CASES]
+
+
+def oracle_chains(case, seed, ids, steps_list):
+    g = case.graph
+    lo, hi = case.bounds
+    hc = np.zeros(g.n_edges + 1, np.uint64)
+    hb = np.zeros(g.n + 1, np.uint64)
+    labs, sts, pops = [], [], []
+    for cid in ids:
+        lab = case.init.copy()
+        st = O.new_stats(1)
+        for steps in steps_list:
+            lab, st, p, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, case.thr, seed, cid,
+                                        steps, stats=st, hist_cut=hc, hist_b=hb)
+        labs.append(lab)
+        sts.append(st[0])
+        pops.append(p)
+    return np.stack(labs), np.array(sts), np.stack(pops), hc, hb
+
+
+def assert_stats_equal(gpu, orc):
+    for f in orc.dtype.names:
+        a, b = gpu[f], orc[f]
+        if f == "sum_invb":
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), (f, a, b)
+        else:
+            assert np.array_equal(a, b), (f, a, b)
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_chain_bit_exact(gpu_lib, case):
+    n_chains, seed, id0 = 6, 2024, 17
+    dg = DeviceGraph(case.graph)
+    assert dg.grid_w == case.graph.grid_w
+    ch = Chains(dg, n_chains, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                base=case.base, seed=seed, chain_id0=id0)
+    steps_list = [700, 1300]  # two launches: state must persist exactly across them
+    for s in steps_list:
+        ch.run(s)
+    labs, st, pops = ch.labels(), ch.stats(), ch.pops()
+    olabs, ost, opops, ohc, ohb = oracle_chains(case, seed, range(id0, id0 + n_chains), steps_list)
+    assert np.array_equal(labs, olabs)
+    assert_stats_equal(st, ost)
+    assert np.array_equal(pops, opops)
+    assert np.array_equal(ch.hist_cut(), ohc)
+    assert np.array_equal(ch.hist_b(), ohb)
+    assert (st["steps"] == sum(steps_list)).all() and not st["stuck"].any()
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c.name in
+                                  ("grid12_k4_pairs", "sec11_a2_k2", "tract_k4")],
+                         ids=lambda c: c.name)
+def test_trace_matches_oracle(gpu_lib, case):
+    dg = DeviceGraph(case.graph)
+    ch = Chains(dg, 3, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                base=case.base, seed=5, chain_id0=0)
+    tr = ch.run_traced(500)
+    lo, hi = case.bounds
+    for cid in range(3):
+        _, _, _, otr = O.run_chain(case.graph, case.init, case.k, case.mode, lo, hi, case.thr, 5,
+                                   cid, 500, trace=True)
+        acc = tr[cid] >= 0
+        assert np.array_equal(np.where(acc, tr[cid] // 64, -1), otr)
+
+
+@pytest.mark.parametrize("name", ["grid10_k2_bi", "grid12_k4_pairs", "sec11_a2_k2", "county_k2",
+                                  "tract_k4", "grid16x24_k8"])
+def test_eval_flips_golden(gpu_lib, name):
+    case = {c.name: c for c in CASES}[name]
+    gold = np.load(os.path.join(GOLDEN, "flips_golden.npz"), allow_pickle=False)
+    lab = gold[f"{name}__labels"]
+    dg = DeviceGraph(case.graph)
+    dcut, contig, pop_ok, db = eval_flips(dg, lab, case.k, gold[f"{name}__v"],
+                                          gold[f"{name}__target"], case.bounds)
+    got = np.stack([dcut, contig, pop_ok, db], 1).astype(np.int32)
+    assert np.array_equal(got, gold[f"{name}__expect"])
+
+
+def test_invalid_initial_state_raises(gpu_lib):
+    from flipcomplexityempirical_amd._lib import InvalidInitialState
+    from flipcomplexityempirical_amd.graph import grid_graph
+    g = grid_graph(6, 6)
+    lab = np.zeros(36, np.int16)
+    lab[[0, 35]] = 1  # district 1 disconnected
+    dg = DeviceGraph(g)
+    with pytest.raises(InvalidInitialState):
+        Chains(dg, 2, 2, lab, proposal="bi", pop_bounds=(0, 36), base=1.0)
+    with pytest.raises(ValueError):  # GerryChain raises ValueError here
+        Chains(dg, 2, 2, lab, proposal="bi", pop_bounds=(0, 36), base=1.0)
+
+
+def test_stuck_flag_instead_of_hang(gpu_lib):
+    """Tight bounds leave no valid flip: the reference would loop forever."""
+    from flipcomplexityempirical_amd.graph import grid_graph, stripe_seed
+    g = grid_graph(6, 6)
+    lab = stripe_seed(6, 6)
+    dg = DeviceGraph(g)
+    ch = Chains(dg, 4, 2, lab, proposal="bi", pop_bounds=(18, 18), base=1.0)
+    ch.run(10, max_retries=50)
+    st = ch.stats()
+    assert st["stuck"].all() and (st["steps"] == 0).all() and (st["attempts"] == 50).all()
+    assert (ch.labels() == lab).all()
