@@ -82,6 +82,8 @@ struct fw_graph {
     g.maxdeg = maxdeg;
     g.gw = gw;
     g.gh = gh;
+    // exact x / gw for x < 2^21 (the grid path is only taken for n < 2^21)
+    g.gmagic = gw ? (((uint64_t)1 << 42) + (uint64_t)gw - 1) / (uint64_t)gw : 0;
     return g;
   }
 };
@@ -231,7 +233,7 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
       }
     }
   }
-  g->gw = detect_grid(g->rowptr, g->col, n);
+  g->gw = n < (1 << 21) ? detect_grid(g->rowptr, g->col, n) : 0;
   g->gh = g->gw ? n / g->gw : 0;
   if (hipSetDevice(device) != hipSuccess) {
     delete g;
@@ -320,13 +322,15 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
 
   // ---- LDS layout
   FwRunParams& p = c->p;
-  p.qcap = 512;
+  p.qcap = 256;
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8);
-  p.off_w = p.lab_bytes;
-  p.off_gsum = p.off_w + round16((int64_t)G * 64 * lb / 8);
-  p.off_pops = p.off_gsum + round16((int64_t)G * 4);
-  p.off_list = p.off_pops + round16((int64_t)k * 8);
+  p.off_gsum = p.lab_bytes;
+  p.off_list = p.off_gsum + round16((int64_t)G * 4);
   p.lds_bytes = p.off_list + p.qcap * 4;
+  if (G > 64 * 16) {
+    delete c;
+    return fail(FW_EUNSUPPORTED, "graph too large (%d weight groups > 1024)", G);
+  }
   if (p.lds_bytes > 160 * 1024 - 64) {
     delete c;
     return fail(FW_EUNSUPPORTED, "graph too large for LDS-resident chains (%d B)", p.lds_bytes);
@@ -562,7 +566,7 @@ int fw_eval_flips(fw_graph* g, const int16_t* labels, int32_t k, const int32_t* 
       return fail(FW_EINVAL, "flip %d (v=%d, target=%d) is not a relabelling", i, v[i], target[i]);
   }
   FwEvalParams p{};
-  p.qcap = 512;
+  p.qcap = 256;
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8);
   p.off_list = p.lab_bytes;
   p.lds_bytes = p.off_list + p.qcap * 4;

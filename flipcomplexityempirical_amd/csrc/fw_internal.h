@@ -18,6 +18,7 @@ struct FwGraphDev {
   const int64_t* pop;     // [n] or nullptr (unit populations)
   int32_t n, nedges, maxdeg;
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)
+  uint64_t gmagic;        // ceil(2^42 / gw): x / gw == (x * gmagic) >> 42 for x < 2^21
 };
 
 struct FwRunParams {
@@ -42,7 +43,7 @@ struct FwRunParams {
   int32_t qcap;                // search-list entries held in LDS
   // LDS layout (bytes from the dynamic shared base)
   int32_t lab_bytes;           // packed label bytes (multiple of 16)
-  int32_t off_w, off_gsum, off_pops, off_list, lds_bytes;
+  int32_t off_gsum, off_list, lds_bytes;
 };
 
 struct FwEvalParams {
