@@ -323,7 +323,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   // ---- LDS layout
   FwRunParams& p = c->p;
   p.qcap = 256;
-  p.lab_bytes = round16(((int64_t)n * lb + 7) / 8);
+  // +8: the grid kernels read label dwords one past the last node
+  p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
   p.off_gsum = p.lab_bytes;
   p.off_list = p.off_gsum + round16((int64_t)G * 4);
   p.lds_bytes = p.off_list + p.qcap * 4;
@@ -392,7 +393,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
                 hipSuccess &&
             hipMalloc(&c->d_hist_b, sizeof(unsigned long long) * (n + 1 + FW_HIST_PAD)) ==
                 hipSuccess &&
-            hipMalloc(&c->d_spill, sizeof(uint32_t) * (size_t)c->grid * n) == hipSuccess &&
+            hipMalloc(&c->d_spill, sizeof(uint32_t) * (size_t)c->grid * (p.use16 ? 4 : 1) * n) ==
+                hipSuccess &&
             hipMalloc(&c->d_next, sizeof(int32_t)) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess;

@@ -44,6 +44,8 @@ struct FwRunParams {
   // LDS layout (bytes from the dynamic shared base)
   int32_t lab_bytes;           // packed label bytes (multiple of 16)
   int32_t off_gsum, off_list, lds_bytes;
+  int32_t slot_stride;         // grid16 kernel: bytes between the four chain slots
+  int32_t use16;               // 1: launch the four-chains-per-wave grid kernel
 };
 
 struct FwEvalParams {
@@ -67,4 +69,7 @@ struct FwEvalParams {
 // Host-side launchers implemented in fw_kernels.hip.
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
-int fw_run_grid_size(const FwRunParams& p, int lb, int device, int* grid);
+int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);
+// fw_grid16.hip
+bool fw_grid16_supported(const FwRunParams& p, int lb);
+void* fw_grid16_fn(const FwRunParams& p);

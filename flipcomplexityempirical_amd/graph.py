@@ -226,6 +226,14 @@ def block_seed(h: int, w: int, brows: int, bcols: int) -> np.ndarray:
     return (i * bcols + j).astype(np.int16).reshape(-1)
 
 
+def band_seed(h: int, w: int, k: int) -> np.ndarray:
+    """Rows split into k horizontal bands of (nearly) equal height, labelled 0..k-1."""
+    if k > h:
+        raise ValueError("need at least one row per band")
+    band = (np.arange(h) * k) // h
+    return np.repeat(band[:, None], w, axis=1).astype(np.int16).reshape(-1)
+
+
 def stripe_seed(h: int, w: int) -> np.ndarray:
     """Rows i >= h/2 -> 1, else 0 (the sec11 'alignment 0' analogue used for C1)."""
     return (np.arange(h)[:, None] >= h // 2).repeat(w, axis=1).astype(np.int16).reshape(-1)

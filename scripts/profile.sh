@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 passes over a short C3 bench: kernel trace + stats, then PMC passes
+# (separate runs; no --pmc together with any trace domain).  Output: gpurun_out/prof_<tag>/
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}
+shift
+BENCH_ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --inner 1000 --no-cpu-baseline"}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 bench.py $BENCH_ARGS > $OUT/ktrace_bench.log 2>&1 || { echo "ktrace failed rc=$?"; tail -20 $OUT/ktrace_bench.log; exit 1; }
+tail -1 $OUT/ktrace_bench.log
+PB="--steps 1 --warmup 1 --inner 500 --no-cpu-baseline"
+i=0
+for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
+            "SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_BRANCH" \
+            "FETCH_SIZE GRBM_GUI_ACTIVE" \
+            "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" ; do
+  i=$((i+1))
+  timeout -s KILL 150 rocprofv3 --pmc $CTRS -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $PB > $OUT/pmc${i}_bench.log 2>&1 || { echo "pmc pass $i failed rc=$?"; tail -5 $OUT/pmc${i}_bench.log; exit 1; }
+  echo "pmc pass $i ok"
+done
+find $OUT -name "*.csv" | head -20

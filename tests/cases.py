@@ -15,8 +15,8 @@ from typing import Optional
 import numpy as np
 
 from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
-from flipcomplexityempirical_amd.graph import (Graph, block_seed, grid_graph, sec11_graph,
-                                               sec11_seed, stripe_seed)
+from flipcomplexityempirical_amd.graph import (Graph, band_seed, block_seed, grid_graph,
+                                               sec11_graph, sec11_seed, stripe_seed)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 MU = 2.63815853
@@ -60,6 +60,10 @@ def cases(include_kansas: bool = True):
         Case("grid12_k4_cut", grid_graph(12, 12), block_seed(12, 12, 2, 2), 4, 2, 0.10, 1.5),
         Case("grid20_k4_mu", grid_graph(20, 20), block_seed(20, 20, 2, 2), 4, 1, 0.05, MU),
         Case("grid16x24_k8", grid_graph(16, 24), block_seed(16, 24, 2, 4), 8, 1, 0.10, 1.0),
+        # widths that are not multiples of 4 (node windows wrap into the next grid row)
+        Case("grid7x9_k3_cut", grid_graph(7, 9), band_seed(7, 9, 3), 3, 2, 0.30, 0.7),
+        Case("grid11x13_k4", grid_graph(11, 13), band_seed(11, 13, 4), 4, 1, 0.30, MU),
+        Case("grid30x18_k2_bi", grid_graph(30, 18), band_seed(30, 18, 2), 2, 0, 0.10, 0.4),
     ]
     g11 = sec11_graph()
     out.append(Case("sec11_a2_k2", g11, sec11_seed(g11, 2), 2, 0, 0.05, 0.1))
