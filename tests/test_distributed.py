@@ -1,0 +1,87 @@
+"""Multi-process sharding on CPU (gloo, world_size 2).
+
+The GPU path shards global chain ids over ranks with no data-path collective and
+merges histograms with one all-reduce (flipcomplexityempirical_amd/distributed.py).  Here
+each rank runs its shard on the CPU oracle (the per-rank engine is irrelevant to the
+sharding logic under test), and the merged histograms/stats must be bit-identical to a
+single-process run of all chains: the per-chain Philox key is the global id.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from flipcomplexityempirical_amd.distributed import (gather_stats, merge_histograms,
+                                                     shard_range)
+
+N_TOTAL, STEPS, SEED = 10, 300, 99
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_shard(case, lo, hi):
+    from oracle import oracle as O
+    g = case.graph
+    hc = np.zeros(g.n_edges + 1, np.uint64)
+    hb = np.zeros(g.n + 1, np.uint64)
+    st = np.zeros(hi - lo, O.STATS_DTYPE)
+    for i, cid in enumerate(range(lo, hi)):
+        _, s, _, _ = O.run_chain(g, case.init, case.k, case.mode, *case.bounds, case.thr, SEED, cid,
+                                 STEPS, hist_cut=hc, hist_b=hb)
+        st[i] = s[0]
+    return hc, hb, st
+
+
+def _worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from cases import cases
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    case = {c.name: c for c in cases(include_kansas=False)}["grid12_k4_pairs"]
+    lo, hi = shard_range(N_TOTAL, world, rank)
+    hc, hb, st = _run_shard(case, lo, hi)
+    mhc, mhb = merge_histograms(hc, hb, dist)
+    mst = gather_stats(st, N_TOTAL, dist, lo)
+    if rank == 0:
+        np.savez(out, hc=mhc, hb=mhb, st=mst.view(np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for total in (1, 7, 65536):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_two_rank_merge_is_bit_identical(tmp_path):
+    from cases import cases
+    case = {c.name: c for c in cases(include_kansas=False)}["grid12_k4_pairs"]
+    out = str(tmp_path / "merged.npz")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    hc, hb, st = _run_shard(case, 0, N_TOTAL)
+    assert np.array_equal(got["hc"], hc) and np.array_equal(got["hb"], hb)
+    assert np.array_equal(got["st"], st.view(np.uint8))
+
+
+def test_merge_without_process_group_is_identity():
+    a, b = np.arange(5, dtype=np.uint64), np.arange(3, dtype=np.uint64)
+    x, y = merge_histograms(a, b, None)
+    assert x is a and y is b

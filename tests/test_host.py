@@ -1,0 +1,104 @@
+"""Host-side logic: graph construction, seeds, bounds and Metropolis tables (CPU only)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from cases import GOLDEN, kansas, kansas_seed
+from flipcomplexityempirical_amd.chain import (expected_wait_sum, metropolis_table,
+                                               population_bounds)
+from flipcomplexityempirical_amd.graph import (Graph, band_seed, block_seed, detect_grid,
+                                               grid_graph, sec11_graph, sec11_seed)
+from flipcomplexityempirical_amd.seeds import recursive_tree_part
+from oracle import oracle as O
+
+
+def test_sec11_graph_matches_reference_construction():
+    g = sec11_graph()  # grid_chain_sec11.py:191,236,252-260
+    assert (g.n, g.n_edges, g.maxdeg, g.grid_w) == (1596, 3116, 4, 0)
+    idx = g.index()
+    assert idx[(1, 0)] in g.neighbors(idx[(0, 1)])  # the added corner diagonal
+    for a in (0, 1, 2):
+        lab = sec11_seed(g, a)
+        assert lab.sum() == 798 and O.plan_valid(g, lab, 2, 790, 806)
+
+
+def test_grid_detection():
+    assert grid_graph(7, 9).grid_w == 9 and detect_grid(grid_graph(100, 100)) == 100
+    assert sec11_graph().grid_w == 0
+    g = grid_graph(5, 5)
+    g2 = Graph.from_adjacency(list(range(25)), {i: list(g.neighbors(i)) for i in range(25)})
+    assert g2.grid_w == 5
+
+
+def test_population_bounds_equal_gerrychain_float_semantics():
+    for total, k, p in [(1596, 2, 0.01), (10000, 4, 0.05), (2853118, 18, 0.05), (100, 2, 0.1),
+                        (40000, 8, 0.05), (1530, 2, 0.9)]:
+        lo_i, hi_i = population_bounds(total, k, p)
+        ideal = total / k
+        lo, hi = (1 - p) * ideal, (1 + p) * ideal
+        for pop in range(max(0, lo_i - 50), hi_i + 50):
+            assert (lo <= pop <= hi) == (lo_i <= pop <= hi_i)
+
+
+def test_metropolis_table_is_python_pow():
+    for base in (0.1, 2.63815853, 1.0, 10.0, 1 / 2.63815853 ** 2):
+        thr = metropolis_table(base, 4)
+        for d in range(-4, 5):
+            assert thr[d + 4] == base ** (-d)  # cut_accept: base**(c_old - c_new)
+
+
+def test_expected_wait_sum():
+    st = np.zeros(2, O.STATS_DTYPE)
+    st["sum_invb"] = [0.5, 0.25]
+    st["yields"] = [3, 4]
+    got = expected_wait_sum(st, 10, 2)
+    assert np.allclose(got, [99 * 0.5 - 3, 99 * 0.25 - 4])
+
+
+def test_block_and_band_seeds():
+    b = block_seed(100, 100, 2, 2)
+    assert np.bincount(b).tolist() == [2500] * 4
+    assert np.bincount(band_seed(11, 13, 4)).sum() == 143
+    g = grid_graph(100, 100)
+    assert O.plan_valid(g, b, 4, *population_bounds(10000, 4, 0.05))
+
+
+@pytest.mark.parametrize("unit,n,e,md", [("County20", 105, 263, 8), ("Tract20", 770, 2005, 13),
+                                         ("COUSUB20", 1530, 3808, 16), ("BG20", 2351, 6252, 15)])
+def test_kansas_fixtures(unit, n, e, md):
+    g = kansas(unit)
+    g.validate()
+    assert (g.n, g.n_edges, g.maxdeg) == (n, e, md)
+    assert g.total_pop == 2853118  # Kansas 2010 TOTPOP (All_States_Chain.py:226-230)
+    for k in (2, 4):
+        lab = kansas_seed(unit, k)
+        assert O.plan_valid(g, lab, k, *population_bounds(g.total_pop, k, 0.10))
+
+
+def test_recursive_tree_part_gives_balanced_contiguous_plans():
+    g = kansas("Tract20")
+    for seed in range(3):
+        lab = recursive_tree_part(g, [0, 1, 2], g.total_pop / 3, 0.05, seed=seed)
+        lo, hi = population_bounds(g.total_pop, 3, 0.10)
+        pops = np.bincount(lab, weights=g.pop, minlength=3)
+        # the first k-1 districts are within epsilon of the target by construction
+        assert all(abs(p - g.total_pop / 3) < 0.05 * g.total_pop / 3 for p in pops[:2])
+        assert O.plan_valid(g, lab, 3, 0, g.total_pop)
+
+
+def test_json_loader_casts_string_totpop():
+    p = os.path.join(GOLDEN, "..", "..", "tests", "golden")
+    assert os.path.isdir(p)
+    import json
+    import tempfile
+    data = {"directed": False, "multigraph": False, "graph": [],
+            "nodes": [{"id": 0, "TOTPOP": "5"}, {"id": 1, "TOTPOP": "7"}],
+            "adjacency": [[{"id": 1}], [{"id": 0}]]}
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(data, f)
+    g = Graph.from_json(f.name)
+    os.unlink(f.name)
+    assert g.pop.tolist() == [5, 7] and g.n_edges == 1
+    assert math.isclose(g.total_pop, 12)

@@ -1,0 +1,51 @@
+"""Statistical pins of the chain law against the reference's own published outputs.
+
+Each New_plots/sec11/{alignment}B{int(100*base)}P{int(100*pop)}wait.txt holds
+sum_t geom_wait_t over 100,000 yields of grid_chain_sec11.py's chain (k=2, the 1,596-node
+sec11 graph, slow_reversible_propose_bi, cut_accept).  E[geom_wait | |B|] =
+(N^2-1)/|B| - 1, so each file pins the run's harmonic-mean boundary size.  The oracle
+is run on the same configurations (same seeds, tolerances, bases, 100,000 yields) and
+its Rao-Blackwellised mean wait per yield must agree with the reference's 15-run mean
+within 3 combined standard errors.  Fixture: tests/golden/wait_sec11.json (extracted
+by tests/golden/make_golden.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from cases import GOLDEN
+from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+from flipcomplexityempirical_amd.graph import sec11_graph, sec11_seed
+from oracle import oracle as O
+
+MU = 2.63815853
+POPS = (0.01, 0.05, 0.1, 0.5, 0.9)
+
+
+def _ours(base, runs):
+    g = sec11_graph()
+    M = float(g.n ** 2 - 1)
+    out = []
+    for a, pop in runs:
+        lo, hi = population_bounds(g.n, 2, pop)
+        _, st, _, _ = O.run_chain(g, sec11_seed(g, a), 2, 0, lo, hi,
+                                  metropolis_table(base, g.maxdeg), 7, a * 10 + int(pop * 100),
+                                  99999)
+        out.append((M * st["sum_invb"][0] - st["yields"][0]) / st["yields"][0])
+    return np.array(out)
+
+
+@pytest.mark.parametrize("base,label,runs", [
+    (MU, 263, [(a, p) for a in (0, 1, 2) for p in POPS]),
+    (10.0, 1000, [(a, p) for a in (0, 1, 2) for p in POPS]),
+    (1.0, 100, [(0, 0.05), (1, 0.5), (2, 0.9), (0, 0.9)]),
+])
+def test_sec11_mean_wait_matches_reference(base, label, runs):
+    ref = json.load(open(os.path.join(GOLDEN, "wait_sec11.json")))
+    refv = np.array([r["wait_sum"] / 1e5 for r in ref if r["base_label"] == label])
+    assert len(refv) == 15
+    ours = _ours(base, runs)
+    se = np.sqrt(refv.var(ddof=1) / len(refv) + ours.var(ddof=1) / len(ours))
+    assert abs(ours.mean() - refv.mean()) < 3 * se + 1e-9, (ours.mean(), refv.mean(), se)
