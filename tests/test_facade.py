@@ -1,0 +1,94 @@
+"""GerryChain-shaped façade: host pieces on CPU, the lowered chain on the GPU."""
+import numpy as np
+import pytest
+
+from cases import MU
+from flipcomplexityempirical_amd import markov as gc
+from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+from flipcomplexityempirical_amd.graph import sec11_graph, sec11_seed
+from oracle import oracle as O
+
+
+def sec11_partition(alignment=2, base=0.1):
+    """The reference's set-up, grid_chain_sec11.py:186-342, through the façade."""
+    g = sec11_graph()
+    lab = sec11_seed(g, alignment)
+    cddict = {node: (1 if lab[i] else -1) for i, node in enumerate(g.nodes)}
+    updaters = {"population": gc.Tally("population"), "cut_edges": gc.cut_edges,
+                "b_nodes": gc.b_nodes_bi, "base": lambda p: base, "geom": gc.geom_wait}
+    return g, gc.Partition(g, assignment=cddict, updaters=updaters)
+
+
+def test_partition_updaters_on_host():
+    g, part = sec11_partition()
+    assert part.parts == [-1, 1] and len(part) == 2
+    assert part["population"] == {-1: 798, 1: 798}
+    cut = part["cut_edges"]
+    lab = part.labels
+    e = g.edges()
+    assert len(cut) == int((lab[e[:, 0]] != lab[e[:, 1]]).sum())
+    assert part["b_nodes"] == {x for e_ in cut for x in e_}
+    node = next(iter(part["b_nodes"]))
+    child = part.flip({node: -part.assignment[node]})
+    assert child.parent is part and child.flips == {node: -part.assignment[node]}
+    assert child.assignment[node] == -part.assignment[node]
+
+
+def test_bounds_and_validator():
+    g, part = sec11_partition()
+    pb = gc.within_percent_of_ideal_population(part, 0.01)
+    assert pb.bounds == (0.99 * 798, 1.01 * 798) and pb(part)
+    assert population_bounds(1596, 2, 0.01) == (791, 805)
+    with pytest.raises(TypeError):
+        gc.Validator([lambda p: 1])(part)
+    assert gc.Validator([lambda p: True, lambda p: False, lambda p: 1])(part) is False
+
+
+def test_unknown_plugins_are_refused():
+    g, part = sec11_partition()
+    pb = gc.within_percent_of_ideal_population(part, 0.05)
+    with pytest.raises(NotImplementedError):
+        gc.MarkovChain(lambda p: p, gc.Validator([gc.single_flip_contiguous, pb]),
+                       gc.cut_accept, part, 10)
+    with pytest.raises(NotImplementedError):
+        gc.MarkovChain(gc.slow_reversible_propose_bi, [gc.single_flip_contiguous, pb],
+                       lambda p: True, part, 10)
+    with pytest.raises(NotImplementedError):
+        gc.slow_reversible_propose_bi(part)
+
+
+@pytest.mark.gpu
+def test_reference_script_shape_runs_on_gpu(gpu_lib):
+    g, part = sec11_partition(alignment=2, base=0.1)
+    pb = gc.within_percent_of_ideal_population(part, 0.05)
+    chain = gc.MarkovChain(gc.slow_reversible_propose_bi,
+                           gc.Validator([gc.single_flip_contiguous, pb]), accept=gc.cut_accept,
+                           initial_state=part, total_steps=1500, seed=5, chain_id=3, chunk=600)
+    parts = list(chain)
+    assert len(parts) == 1500 and parts[0] is part
+    # the reference re-yields the same object after a Metropolis rejection
+    assert any(a is b for a, b in zip(parts, parts[1:]))
+    lo, hi = population_bounds(g.n, 2, 0.05)
+    olab, ost, _, otr = O.run_chain(g, sec11_seed(g, 2), 2, 0, lo, hi, metropolis_table(0.1, 4),
+                                    5, 3, 1499, trace=True)
+    assert np.array_equal(parts[-1].labels, olab)
+    # the per-yield observables of grid_chain_sec11.py:367-369 agree with the oracle's sums
+    assert sum(len(p["cut_edges"]) for p in parts) == int(ost["sum_cut"][0])
+    assert sum(len(p["b_nodes"]) for p in parts) == int(ost["sum_bnodes"][0])
+    # single_flip_contiguous on a yielded child agrees (evaluated by the GPU eval kernel)
+    child = next(p for p in parts[1:] if p.parent is not None)
+    assert gc.single_flip_contiguous(child) is True
+
+
+@pytest.mark.gpu
+def test_run_batched_matches_oracle(gpu_lib):
+    g, part = sec11_partition(alignment=0, base=MU)
+    pb = gc.within_percent_of_ideal_population(part, 0.10)
+    chain = gc.MarkovChain(gc.slow_reversible_propose_bi, [gc.single_flip_contiguous, pb],
+                           gc.MetropolisCutAccept(MU), part, 1001, seed=9)
+    res = chain.run_batched(5, chain_id0=100)
+    lo, hi = population_bounds(g.n, 2, 0.10)
+    for i in range(5):
+        olab, _, _, _ = O.run_chain(g, sec11_seed(g, 0), 2, 0, lo, hi, metropolis_table(MU, 4), 9,
+                                    100 + i, 1000)
+        assert np.array_equal(res.labels[i], olab)
