@@ -152,6 +152,39 @@ __device__ __forceinline__ void lds_add(LDS uint32_t* p, uint32_t v) {
 
 constexpr uint32_t NOLAB = 0xFFFFu;  // label of an absent cell (never a district or code)
 
+// Second-level local contiguity test on the 7x7 window centred at v (bit i*7+j, v = bit
+// 24, A = a-labelled in-grid window cells except v).  1: every a-neighbour of v lies in
+// one window component (connected); 0: some source's window component touches no border
+// cell, i.e. it is a closed component of (district minus v) missing a source
+// (disconnected); -1: undecided.  Identical to orc_window_verdict (the oracle).
+__device__ __forceinline__ int window_verdict(uint64_t A) {
+  const uint64_t C0 = 0x0040810204081ull, C6 = C0 << 6;
+  const uint64_t BORDER = C0 | C6 | 0x7Full | (0x7Full << 42);
+  const uint64_t src = A & ((1ull << 17) | (1ull << 23) | (1ull << 25) | (1ull << 31));
+  uint64_t covered = 0;
+  int verdict = -1;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int sb = s == 0 ? 17 : s == 1 ? 23 : s == 2 ? 25 : 31;
+    const uint64_t b = 1ull << sb;
+    if (verdict >= 0 || !(src & b) || (covered & b)) continue;
+    uint64_t x = b;
+    for (;;) {
+      const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
+      if (y == x) break;
+      x = y;
+    }
+    if ((x & src) == src)
+      verdict = 1;
+    else if (!(x & BORDER))
+      verdict = 0;
+    covered |= x;
+  }
+  return verdict;
+}
+// window cell c in [0,48) (v skipped) -> bit position and (di, dj) offsets from v
+__device__ __forceinline__ int window_pos(int c) { return c < 24 ? c : c + 1; }
+
 // ---------------------------------------------------------------- chain context
 // Grid lane roles for v's neighbourhood: 0 v, 1 up, 2 left, 3 right, 4 down
 // (= CSR order of v's neighbours), 5 NE, 6 SE, 7 SW, 8 NW.
@@ -517,6 +550,18 @@ struct Ctx {
       const int NE = (rb >> 4) & 1, SE = (rb >> 5) & 1, SW = (rb >> 6) & 1, NW = (rb >> 7) & 1;
       const int lNE = pN & pE & NE, lES = pE & pS & SE, lSW = pS & pW & SW, lWN = pW & pN & NW;
       if (m - (lNE + lES + lSW + lWN) <= 1) return true;
+      {  // 7x7 window: lanes 0..47 read one cell each
+        int vr, vc;
+        divmod(v, vr, vc);
+        const int pos = window_pos(lane < 48 ? lane : 0);
+        const int rr = vr - 3 + pos / 7, cc = vc - 3 + pos % 7;
+        const bool in = lane < 48 && rr >= 0 && rr < g.gh && cc >= 0 && cc < g.gw &&
+                        L(rr * g.gw + cc) == a;
+        const uint64_t b48 = ballot(in) & ((1ull << 48) - 1ull);
+        const uint64_t A = (b48 & ((1ull << 24) - 1ull)) | ((b48 >> 24) << 25);
+        const int wv = window_verdict(A);
+        if (wv >= 0) return wv == 1;
+      }
       // pre-merge the ring links; source index of lane l = rank of l among am's bits
       auto sx = [&](int ln) { return __popcll(am & ((1ull << ln) - 1ull)); };
       auto merge = [&](int s1, int s2) {

@@ -18,9 +18,41 @@
 
 #include "fw_device.h"
 
+#ifdef FW_STAMPS
+// Diagnostic build only (libflipwalk_stamps.so): per-phase s_memtime shares.
+__device__ unsigned long long g_stamps[8];
+#define STAMP_DECL uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_t0 = 0;
+#define STAMP(i)                                              \
+  do {                                                        \
+    __builtin_amdgcn_sched_barrier(0);                        \
+    uint64_t st_t1;                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t1)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                        \
+    if (i >= 0) st_acc[(i) < 0 ? 0 : (i)] += st_t1 - st_t0;   \
+    st_t0 = st_t1;                                            \
+  } while (0)
+#define STAMP_FLUSH                                           \
+  if (__lane_id() == 0)                                       \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stamps[i_], (unsigned long long)st_acc[i_]);
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH
+#endif
+
 namespace {
 
 constexpr int ROW = 16;
+
+// v's neighbourhood as one lane sees it (labels < 16 here, so 32-bit label sets)
+struct Hood16 {
+  int x;          // node id, -1 if absent
+  uint32_t lx;    // label of x (NOLAB if absent)
+  uint32_t bits;  // OR of 1<<label over x's neighbours other than v
+  uint32_t cnt;   // number of x's neighbours other than v with label != lx
+  bool has_v;     // v is a neighbour of x
+  int deg;        // degree of x
+};
 
 __device__ __forceinline__ uint32_t rowbits(uint64_t bal, int row) {
   return (uint32_t)(bal >> (row * ROW)) & 0xFFFFu;
@@ -119,6 +151,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
     c = x - r * W;
   };
   __shared__ int32_t s_base;
+  STAMP_DECL
 
   for (;;) {
     if (lane == 0) s_base = atomicAdd(p.next_chain, 4);
@@ -203,18 +236,36 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
     };
     observe(has && !stuck && yields0 == 0 && attempts == 0);
 
+    // Philox batches: lane q of a row holds the draw of its chain's attempt (base + q).
+    // Active rows consume one attempt per loop iteration in lockstep, so every row reads
+    // lane `bpos` of its own row; a row that stops stays stopped for this launch.
+    U4 pb = {0u, 0u, 0u, 0u};
+    int bpos = ROW;
+
     const bool unit_pop = p.g.pop == nullptr;
     for (;;) {
+      STAMP(-1);
       // ---- who proposes this round
       if (!stuck && (retries >= (uint32_t)p.max_retries || npairs == 0)) stuck = 1;
       const bool act = has && !stuck && (int64_t)n_steps < p.steps;
       if (ballot(act) == 0ull) break;
 
-      const U4 x = philox((uint32_t)attempts, (uint32_t)(attempts >> 32), (uint32_t)gid,
-                          (uint32_t)(gid >> 32), key0, key1);
+      if (bpos == ROW) {
+        const uint64_t t = attempts + (uint64_t)q;
+        pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), key0,
+                    key1);
+        bpos = 0;
+      }
+      const int src = (row * ROW + bpos) * 4;  // ds_bpermute byte address of the source lane
+      const U4 x = {(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x0),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x1),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x2),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x3)};
+      ++bpos;
       attempts += act ? 1u : 0u;
       const uint32_t r = scale64(x.x0, x.x1, (uint32_t)(npairs > 0 ? npairs : 1));
 
+      STAMP(0);  // draw
       // ---- select, level 1: group sums (PER per lane)
       uint32_t gs[PER];
       uint32_t s = 0;
@@ -245,6 +296,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
       const int gi = min((int)(pk1 >> 16), G - 1);
       const uint32_t r1 = pk1 & 0xFFFFu;
 
+      STAMP(1);  // level 1
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
@@ -272,12 +324,13 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
       if (act && (rb1 == 0 || rb2 == 0)) stuck = 2;  // inconsistent state: flag, stop chain
       const bool go = act && rb1 != 0 && rb2 != 0;
 
+      STAMP(2);  // level 2
       // ---- v's neighbourhood: row-lane roles 0 v, 1 up, 2 left, 3 right, 4 down,
       //      5 NE, 6 SE, 7 SW, 8 NW; lanes 0..4 also read their node's neighbours
       int vr, vc;
       divmod(v, vr, vc);
       const int dv = (vr > 0) + (vc > 0) + (vc < W - 1) + (vr < H - 1);
-      Hood h;
+      Hood16 h;
       h.x = -1;
       h.lx = NOLAB;
       h.bits = 0;
@@ -305,7 +358,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
                 continue;
               }
               const uint32_t ly = P::get(lab, y);
-              h.bits |= 1ull << ly;
+              h.bits |= 1u << ly;
               h.cnt += ly != h.lx;
             }
           }
@@ -342,6 +395,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
                        ((uint32_t)q == d && pops + pv > p.pop_hi);
       const bool pop_ok = rowbits(ballot(bad), row) == 0u;
 
+      STAMP(3);  // gather, target, Δcut, population
       // ---- contiguity: 8-cell ring test, exact race search when inconclusive
       const uint32_t rbits8 = rowbits(ballot(q >= 1 && q <= 8 && h.lx == a), row) >> 1;
       const int pN = rbits8 & 1, pW = (rbits8 >> 1) & 1, pE = (rbits8 >> 2) & 1, pS = (rbits8 >> 3) & 1;
@@ -349,7 +403,23 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
                 NW = (rbits8 >> 7) & 1;
       const int lNE = pN & pE & NE, lES = pE & pS & SE, lSW = pS & pW & SW, lWN = pW & pN & NW;
       bool contig = m == 1 || (m >= 2 && m - (lNE + lES + lSW + lWN) <= 1);
-      const bool need = go && pop_ok && m >= 2 && !contig;
+      bool need = go && pop_ok && m >= 2 && !contig;
+      if (ballot(need)) {  // 7x7 window flood fill (3 window cells per row-lane)
+        uint64_t A = 0;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int pos = window_pos(q + ROW * t);
+          const int rr = vr - 3 + pos / 7, cc = vc - 3 + pos % 7;
+          const bool in = rr >= 0 && rr < H && cc >= 0 && cc < W && P::get(lab, rr * W + cc) == a;
+          A |= (uint64_t)rowbits(ballot(in), row) << (ROW * t);
+        }
+        A = (A & ((1ull << 24) - 1ull)) | ((A >> 24) << 25);
+        const int wv = need ? window_verdict(A) : -1;
+        if (wv >= 0) {
+          contig = wv == 1;
+          need = false;
+        }
+      }
       uint64_t rows_need = ballot(q == 0 && need);
       while (rows_need) {  // wave-cooperative exact search, one chain slot at a time
         const int L0 = __ffsll((unsigned long long)rows_need) - 1;
@@ -398,6 +468,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
         }
       }
 
+      STAMP(4);  // ring test + exact searches
       // ---- outcome
       const bool valid = go && pop_ok && contig;
       if (go) {
@@ -422,16 +493,16 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
             wo = (uint32_t)(h.deg - m);
             wn = (uint32_t)(h.deg - nbd);
           } else {
-            wo = (uint32_t)__popcll(h.bits & ~(1ull << a));
-            wn = (uint32_t)__popcll(h.bits & ~(1ull << d));
+            wo = (uint32_t)__popc(h.bits & ~(1u << a));
+            wn = (uint32_t)__popc(h.bits & ~(1u << d));
           }
         } else if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
           wo = h.cnt + (h.has_v && a != h.lx);
           wn = h.cnt + (h.has_v && d != h.lx);
         } else {
-          const uint64_t keep = ~(1ull << h.lx);
-          wo = (uint32_t)__popcll((h.bits | (h.has_v ? 1ull << a : 0ull)) & keep);
-          wn = (uint32_t)__popcll((h.bits | (h.has_v ? 1ull << d : 0ull)) & keep);
+          const uint32_t keep = ~(1u << h.lx);
+          wo = (uint32_t)__popc((h.bits | (h.has_v ? 1u << a : 0u)) & keep);
+          wn = (uint32_t)__popc((h.bits | (h.has_v ? 1u << d : 0u)) & keep);
         }
       }
       if (accepted) {
@@ -455,8 +526,10 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
         if ((uint32_t)q == d) pops += pv;
       }
       observe(valid);
+      STAMP(5);  // outcome, Metropolis, commit, observe
     }
 
+    STAMP(6);  // loop exit
     // ---- write back
     if (has) {
       if (hc0) atomicAdd(p.hist_cut + base_c + q, (unsigned long long)hc0);
@@ -491,6 +564,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
     }
     __syncthreads();
   }
+  STAMP_FLUSH
 }
 
 template <int MODE>
@@ -502,6 +576,18 @@ void* pick16(int G) {
 }
 
 }  // namespace
+
+#ifdef FW_STAMPS
+extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 bool fw_grid16_supported(const FwRunParams& p, int lb) {
   return p.g.gw > 0 && lb == 4 && p.G <= 16 * 16 && p.k <= 15 && p.g.maxdeg == 4;

@@ -218,6 +218,49 @@ static int32_t grid_ring(const chain_t* c, int32_t v, int16_t a, const int32_t* 
   return comps < 1 ? 1 : comps;
 }
 
+/* Grid second-level local test on the 7x7 window centred at v (bit i*7+j, v = bit 24):
+ * flood-fill the a-labelled window cells (v excluded) from each of v's a-neighbours.
+ * Returns 1 if all of them lie in one window component (connected), 0 if some source's
+ * component touches no window border cell (a closed component of A minus v that misses a
+ * source: disconnected), -1 otherwise (undecided: the full search decides).  A pure
+ * function of the window, implemented identically by the kernels (fw_device.h). */
+int orc_window_verdict(uint64_t A) {
+  const uint64_t C0 = 0x0040810204081ull;       /* j == 0 */
+  const uint64_t C6 = C0 << 6;                  /* j == 6 */
+  const uint64_t R0 = 0x7Full, R6 = 0x7Full << 42;
+  const uint64_t BORDER = C0 | C6 | R0 | R6;
+  const int sbit[4] = {17, 23, 25, 31};         /* up, left, right, down */
+  uint64_t src = 0;
+  for (int s = 0; s < 4; ++s) src |= A & (1ull << sbit[s]);
+  uint64_t covered = 0;
+  for (int s = 0; s < 4; ++s) {
+    const uint64_t b = 1ull << sbit[s];
+    if (!(src & b) || (covered & b)) continue;
+    uint64_t x = b;
+    for (;;) {
+      const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
+      if (y == x) break;
+      x = y;
+    }
+    if ((x & src) == src) return 1;
+    if (!(x & BORDER)) return 0;
+    covered |= x;
+  }
+  return -1;
+}
+
+static uint64_t window_mask(const chain_t* c, int32_t v, int16_t a) {
+  const int32_t W = c->g.grid_w, H = c->g.grid_h, r = v / W, q = v % W;
+  uint64_t A = 0;
+  for (int i = 0; i < 7; ++i)
+    for (int j = 0; j < 7; ++j) {
+      const int32_t rr = r - 3 + i, cc = q - 3 + j;
+      if ((i == 3 && j == 3) || rr < 0 || rr >= H || cc < 0 || cc >= W) continue;
+      if (c->lab[rr * W + cc] == a) A |= 1ull << (i * 7 + j);
+    }
+  return A;
+}
+
 static int contiguous_after(chain_t* c, int32_t v, int16_t a, int count) {
   const graph_t* g = &c->g;
   int32_t src[64];
@@ -229,6 +272,8 @@ static int contiguous_after(chain_t* c, int32_t v, int16_t a, int count) {
   if (m == 1) return 1;
   if (g->grid_w) {
     if (grid_ring(c, v, a, src, m, uf) == 1) return 1;
+    const int wv = orc_window_verdict(window_mask(c, v, a));
+    if (wv >= 0) return wv;
   } else {
     for (int32_t i = 0; i < m; ++i) uf[i] = i;
   }
