@@ -114,8 +114,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
-                    help="per-launch HBM bytes from a rocprofv3 PMC pass (profiles/)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
+                    help="per-launch HBM bytes from a rocprofv3 PMC pass of the default C3 "
+                         "command (scripts/profile.sh -> scripts/pmc_summary.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,7 +175,8 @@ def main():
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
+    default_c3 = (n, k, args.chains, args.inner, args.proposal) == (100, 4, 65536, 1000, "pairs")
+    if default_c3 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 

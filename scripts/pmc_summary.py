@@ -1,15 +1,27 @@
-"""Summarise a profile.sh output directory: kernel stats + per-dispatch PMC means."""
+"""Summarise a profile.sh output directory: kernel stats + per-dispatch PMC means.
+
+    python scripts/pmc_summary.py gpurun_out/prof_<tag> [traffic.json]
+
+With a second argument, writes the per-launch HBM traffic of the chain kernel as JSON
+(bench.py --traffic-json reads it): FETCH_SIZE and WRITE_SIZE are kilobytes; on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM), so
+it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores (the state write-back).
+"""
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
 d = sys.argv[1]
 ks = os.path.join(d, "ktrace", "run_kernel_stats.csv")
+kern = {}
 if os.path.exists(ks):
     for r in csv.DictReader(open(ks)):
         print(f"{r['Name'][:70]:70s} calls={r['Calls']:>4s} avg_ms={float(r['AverageNs'])/1e6:9.3f}")
+        if "fw_" in r["Name"]:
+            kern = {"name": r["Name"], "avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"])}
 agg = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
@@ -17,3 +29,13 @@ for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg.items()):
     print(f"{k:28s} {sum(v)/len(v):16.4g}  (n={len(v)})")
+if len(sys.argv) > 2 and "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
+    fetch = sum(agg["FETCH_SIZE"]) / len(agg["FETCH_SIZE"]) * 1024.0
+    write = sum(agg["WRITE_SIZE"]) / len(agg["WRITE_SIZE"]) * 1024.0
+    out = {"hbm_bytes_per_launch": 2.0 * fetch + write, "fetch_bytes_raw": fetch,
+           "fetch_bytes_corrected": 2.0 * fetch, "write_bytes": write,
+           "source": os.path.basename(os.path.normpath(d)), "kernel_trace": kern,
+           "note": "FETCH_SIZE x2 (gfx950 coalesced-read correction) + WRITE_SIZE, KB->B"}
+    with open(sys.argv[2], "w") as f:
+        json.dump(out, f, indent=1)
+    print("traffic ->", sys.argv[2], out["hbm_bytes_per_launch"])

@@ -47,20 +47,18 @@ def assert_stats_equal(gpu, orc):
             assert np.array_equal(a, b), (f, a, b)
 
 
-@pytest.fixture(params=["auto", "wave64"])
-def kernel_path(request, monkeypatch):
-    """auto: four-chains-per-wave kernel on grids; wave64: force one chain per wave."""
-    if request.param == "wave64":
+# auto: the four-chains-per-wave kernel on grids; wave64: force one chain per wave.
+# CSR graphs always run the one-chain-per-wave kernel, so they appear once.
+KERNEL_CASES = [(c, p) for c in CASES for p in ("auto", "wave64") if p == "auto" or c.graph.grid_w]
+
+
+@pytest.mark.parametrize("case,kernel_path", KERNEL_CASES,
+                         ids=[f"{p}-{c.name}" for c, p in KERNEL_CASES])
+def test_chain_bit_exact(gpu_lib, case, kernel_path, monkeypatch):
+    if kernel_path == "wave64":
         monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
     else:
         monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
-    return request.param
-
-
-@pytest.mark.parametrize("case", CASES, ids=IDS)
-def test_chain_bit_exact(gpu_lib, case, kernel_path):
-    if kernel_path == "wave64" and not case.graph.grid_w:
-        pytest.skip("CSR graphs always use the one-chain-per-wave kernel")
     n_chains, seed, id0 = 7, 2024, 17
     dg = DeviceGraph(case.graph)
     assert dg.grid_w == case.graph.grid_w
