@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -59,6 +60,15 @@ int detect_grid(const std::vector<int32_t>& rp, const std::vector<int32_t>& col,
       e += d;
     }
   return w;
+}
+
+// Entries of a contiguity search's visit list held in LDS before it spills to HBM.
+// FLIPWALK_LIST_CAP overrides it (tests force the spill path with a tiny cap).
+int list_cap(int dflt) {
+  const char* e = getenv("FLIPWALK_LIST_CAP");
+  if (!e || !e[0]) return dflt;
+  const int v = atoi(e);
+  return v >= 1 ? v : dflt;
 }
 
 }  // namespace
@@ -115,21 +125,17 @@ int pick_lb(int k, int maxdeg) {
   return 0;
 }
 
+// LB-bit little-endian fields: node x in bits [x*LB, x*LB + LB) of the byte stream.
 void pack_labels(const int16_t* lab, int n, int lb, uint8_t* out, int bytes) {
   std::memset(out, 0, (size_t)bytes);
-  if (lb == 8) {
-    for (int x = 0; x < n; ++x) out[x] = (uint8_t)lab[x];
-  } else {
-    for (int x = 0; x < n; ++x) out[x >> 1] |= (uint8_t)((lab[x] & 15) << ((x & 1) * 4));
-  }
+  const int per = 8 / lb;
+  for (int x = 0; x < n; ++x)
+    out[x / per] |= (uint8_t)((lab[x] & ((1 << lb) - 1)) << ((x % per) * lb));
 }
 
 void unpack_labels(const uint8_t* in, int n, int lb, int16_t* lab) {
-  if (lb == 8) {
-    for (int x = 0; x < n; ++x) lab[x] = in[x];
-  } else {
-    for (int x = 0; x < n; ++x) lab[x] = (in[x >> 1] >> ((x & 1) * 4)) & 15;
-  }
+  const int per = 8 / lb;
+  for (int x = 0; x < n; ++x) lab[x] = (in[x / per] >> ((x % per) * lb)) & ((1 << lb) - 1);
 }
 
 // MarkovChain's initial-state validity: every district non-empty, connected and
@@ -307,10 +313,14 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     return fail(FW_EINVAL, "slow_reversible_propose_bi needs k == 2 (got %d)", k);
   if (g->maxdeg > FW_MAX_DEG)
     return fail(FW_EUNSUPPORTED, "max degree %d > %d", g->maxdeg, FW_MAX_DEG);
-  const int lb = pick_lb(k, g->maxdeg);
-  if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
   const int n = g->n, D = g->maxdeg;
   const int G = (n + 63) / 64;
+  // row-major grids: the four-chains-per-wave kernel, 2-bit labels when k <= 4
+  // (FLIPWALK_NO_GRID16=1 forces the one-chain-per-wave kernel, for A/B parity tests)
+  const char* no16 = getenv("FLIPWALK_NO_GRID16");
+  const bool use16 = fw_grid16_candidate(g->gw, D, G, k) && !(no16 && no16[0] == '1');
+  const int lb = use16 ? (k <= 4 ? 2 : 4) : pick_lb(k, g->maxdeg);
+  if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 
   auto c = new fw_chains();
   c->g = g;
@@ -322,7 +332,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
 
   // ---- LDS layout
   FwRunParams& p = c->p;
-  p.qcap = 256;
+  p.qcap = list_cap(256);
+  p.qcap16 = list_cap(384);
   // +8: the grid kernels read label dwords one past the last node
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
   p.off_gsum = p.lab_bytes;
@@ -380,9 +391,12 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.chain_id0 = chain_id0;
   p.lab_stride = lab_stride;
   p.thr_stride = thr_per_chain ? 2 * D + 1 : 0;
-  if (fw_run_grid_size(p, lb, g->device, &c->grid) != 0) {
+  p.lb = lb;
+  p.use16 = use16 ? 1 : 0;
+  if ((use16 ? fw_grid16_plan(p, g->device, &c->grid)
+             : fw_run_grid_size(p, lb, g->device, &c->grid)) != 0) {
     delete c;
-    return fail(FW_EHIP, "occupancy query failed (LDS %d B)", p.lds_bytes);
+    return fail(FW_EHIP, "occupancy query failed (LDS %d B)", use16 ? p.lds16 : p.lds_bytes);
   }
   const size_t nthr = (size_t)(thr_per_chain ? n_chains : 1) * (2 * D + 1);
   bool ok = hipMalloc(&c->d_labels, packed.size()) == hipSuccess &&
@@ -393,7 +407,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
                 hipSuccess &&
             hipMalloc(&c->d_hist_b, sizeof(unsigned long long) * (n + 1 + FW_HIST_PAD)) ==
                 hipSuccess &&
-            hipMalloc(&c->d_spill, sizeof(uint32_t) * (size_t)c->grid * (p.use16 ? 4 : 1) * n) ==
+            hipMalloc(&c->d_spill, sizeof(uint32_t) * (size_t)c->grid * n) ==
                 hipSuccess &&
             hipMalloc(&c->d_next, sizeof(int32_t)) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -568,7 +582,7 @@ int fw_eval_flips(fw_graph* g, const int16_t* labels, int32_t k, const int32_t* 
       return fail(FW_EINVAL, "flip %d (v=%d, target=%d) is not a relabelling", i, v[i], target[i]);
   }
   FwEvalParams p{};
-  p.qcap = 256;
+  p.qcap = list_cap(256);
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8);
   p.off_list = p.lab_bytes;
   p.lds_bytes = p.off_list + p.qcap * 4;

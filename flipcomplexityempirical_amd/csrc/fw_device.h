@@ -118,8 +118,11 @@ struct PK {
   __device__ static __forceinline__ uint32_t get(const LDS uint8_t* b, int x) {
     if constexpr (LB == 8) {
       return b[x];
-    } else {
+    } else if constexpr (LB == 4) {
       return (uint32_t)(b[x >> 1] >> ((x & 1) << 2)) & 15u;
+    } else {
+      static_assert(LB == 2, "labels are 2, 4 or 8 bits");
+      return (uint32_t)(b[x >> 2] >> ((x & 3) << 1)) & 3u;
     }
   }
   __device__ static __forceinline__ LDS uint32_t* word(LDS uint8_t* b, int x) {

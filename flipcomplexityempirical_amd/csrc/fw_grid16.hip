@@ -1,19 +1,24 @@
-// fw_grid16.hip — the row-major-grid chain kernel, four chains per wavefront.
+// fw_grid16.hip — the row-major-grid chain kernel: four chains per wavefront, 1-4
+// wavefronts per workgroup.
 //
-// The one-chain-per-wave kernel (fw_kernels.hip) is bound by the CU's scalar unit:
-// per proposal it issues ~340 scalar instructions (Philox on the SALU plus the exec-
-// mask bookkeeping of lane-role branches) for one chain.  Here each 16-lane DPP row
-// of a wavefront owns one chain, so every instruction of the common path serves four
-// chains: Philox runs on the VALU, per-chain scalars live in row-uniform VGPRs,
-// prefix scans are 4-step row_shr DPP scans, a lane's value is broadcast to its row
-// by a masked row scan + row_newbcast, and row-level votes are bit fields of one
-// 64-bit ballot.  The exact contiguity search (needed by a few percent of proposals)
-// runs wave-cooperatively on one chain slot at a time with the shared race search of
-// fw_device.h, so its result is the same bit for bit as in the other kernel.
+// The chain loop is latency-bound (one dependent LDS round trip or DPP chain per
+// phase, no phase dominant), so throughput follows the number of chains resident per
+// CU, which LDS sets.  Each 16-lane DPP row of a wavefront owns one chain, so every
+// instruction of the common path serves four chains: Philox runs on the VALU,
+// per-chain scalars live in row-uniform VGPRs, prefix scans are 4-step row_shr DPP
+// scans, a lane's value is broadcast to its row by a masked row scan + row_newbcast,
+// and row-level votes are bit fields of one 64-bit ballot.
 //
-// LDS: four chain slots (labels | group sums), slot stride padded so the four rows
-// start on different banks, then one search list shared by the four chains.
-// Semantics: oracle/flipchain_oracle.c.
+// Per chain, LDS holds only the packed labels (2 bits/node when k <= 4, else 4) and a
+// u16 proposal-weight sum per 64-node group (C3, 100x100 k=4: 2,832 B).  The exact
+// contiguity search (needed by <1% of proposals) runs wave-cooperatively on one chain
+// at a time and marks visited nodes in a 4-bit scratch array shared by the
+// workgroup's waves (held under an LDS lock), together with one shared visit list.
+// Its level-synchronous race is the one of fw_device.h / the oracle, so verdicts and
+// search counters match bit for bit.
+//
+// Semantics: oracle/flipchain_oracle.c (chain loop, proposals, contiguity, accept,
+// observables), reference grid_chain_sec11.py:117-179,340-402.
 #include <hip/hip_runtime.h>
 
 #include "fw_device.h"
@@ -43,6 +48,8 @@ __device__ unsigned long long g_stamps[8];
 namespace {
 
 constexpr int ROW = 16;
+constexpr int MAX_NW = 4;          // waves per workgroup
+constexpr uint32_t SCR_BLOCK = 15;  // scratch code of v during a search
 
 // v's neighbourhood as one lane sees it (labels < 16 here, so 32-bit label sets)
 struct Hood16 {
@@ -75,36 +82,34 @@ __device__ __forceinline__ uint32_t row_pick(uint32_t x, int L, int q) {
   return row_sum(q == L ? x : 0u);
 }
 
-// Four consecutive nibbles x..x+3 of a packed 4-bit label array (16 bits), plus the
-// nibbles at x-1 and x+4 (returned in bits 16..19 and 20..23).  Two aligned dword
+// Labels of the six consecutive nodes x-1 .. x+4 of a packed LB-bit label array, LB
+// bits each (field 0 = x-1, fields 1..4 = x..x+3, field 5 = x+4).  Two aligned dword
 // reads; the label region is padded so the second read stays inside the slot.
-__device__ __forceinline__ uint32_t nib_window(const LDS uint8_t* lab, int x) {
-  const int xm = x - 1;  // may be -1: then the low nibble is garbage and masked by callers
-  const int bit = xm * 4;
-  const int wi = bit >> 5;  // dword holding nibble xm (arithmetic shift: -1 -> -1)
+template <int LB>
+__device__ __forceinline__ uint32_t lab_window(const LDS uint8_t* lab, int x) {
+  const int bit = (x - 1) * LB;  // x - 1 may be -1: field 0 is then garbage, masked by callers
+  const int wi = bit >> 5;       // arithmetic shift: -1 -> -1
   const LDS uint32_t* w = reinterpret_cast<const LDS uint32_t*>(lab);
   const uint32_t lo = wi >= 0 ? w[wi] : 0u;
   const uint32_t hi = w[wi + 1];
   const uint64_t both = ((uint64_t)hi << 32) | lo;
-  const uint32_t sh = (uint32_t)(bit - wi * 32);
-  const uint32_t six = (uint32_t)(both >> sh) & 0xFFFFFFu;  // nibbles xm .. xm+5
-  // reorder: own 4 nibbles in bits 0..15, x-1 in 16..19, x+4 in 20..23
-  return ((six >> 4) & 0xFFFFu) | ((six & 0xFu) << 16) | (((six >> 20) & 0xFu) << 20);
+  return (uint32_t)(both >> (uint32_t)(bit - wi * 32)) & ((1u << (6 * LB)) - 1u);
 }
 
 // Proposal weights (and cut degrees) of the four nodes x0..x0+3 (x0 a multiple of 4)
 // of a row-major W x H grid, packed one per byte.  A window may wrap into the next grid
 // row when W is not a multiple of 4, so neighbour windows are read whenever ANY of the
 // four nodes has that neighbour; per-node row/column checks mask the rest.
-template <int MODE>
+template <int LB, int MODE>
 __device__ __forceinline__ void weights4(const LDS uint8_t* lab, int x0, int W, int H, int n,
                                          uint64_t gmagic, uint32_t& w4, uint32_t& cd4) {
+  constexpr uint32_t M = (1u << LB) - 1u;
   w4 = 0;
   cd4 = 0;
   if (x0 >= n) return;
-  const uint32_t own = nib_window(lab, x0);
-  const uint32_t up = x0 + 3 - W >= 0 ? nib_window(lab, x0 - W) : 0u;
-  const uint32_t dn = x0 + W < n ? nib_window(lab, x0 + W) : 0u;
+  const uint32_t own = lab_window<LB>(lab, x0);
+  const uint32_t up = x0 + 3 - W >= 0 ? lab_window<LB>(lab, x0 - W) : 0u;
+  const uint32_t dn = x0 + W < n ? lab_window<LB>(lab, x0 + W) : 0u;
   const int r0 = (int)(((uint64_t)(uint32_t)x0 * gmagic) >> 42);
   const int c0 = x0 - r0 * W;
 #pragma unroll
@@ -114,10 +119,10 @@ __device__ __forceinline__ void weights4(const LDS uint8_t* lab, int x0, int W, 
       ct -= W;
       rt += 1;
     }
-    const uint32_t lx = (own >> (4 * tt)) & 15u;
-    const uint32_t ll = tt == 0 ? (own >> 16) & 15u : (own >> (4 * tt - 4)) & 15u;
-    const uint32_t lr = tt == 3 ? (own >> 20) & 15u : (own >> (4 * tt + 4)) & 15u;
-    const uint32_t lu = (up >> (4 * tt)) & 15u, ld = (dn >> (4 * tt)) & 15u;
+    const uint32_t lx = (own >> (LB * (tt + 1))) & M;
+    const uint32_t ll = (own >> (LB * tt)) & M;
+    const uint32_t lr = (own >> (LB * (tt + 2))) & M;
+    const uint32_t lu = (up >> (LB * (tt + 1))) & M, ld = (dn >> (LB * (tt + 1))) & M;
     uint32_t bits = 0, cd = 0;
     if (rt > 0) { bits |= 1u << lu; cd += lu != lx; }
     if (ct > 0) { bits |= 1u << ll; cd += ll != lx; }
@@ -134,29 +139,161 @@ __device__ __forceinline__ uint32_t bsum4(uint32_t v) {
   return (v & 0xFFu) + ((v >> 8) & 0xFFu) + ((v >> 16) & 0xFFu) + (v >> 24);
 }
 
-template <int MODE, int PER>
-__global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
+// 4-bit scratch field x := 0 (atomic on the shared word)
+__device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
+  __atomic_fetch_and(PK<4>::word(scr, x), ~(15u << PK<4>::shift(x)), __ATOMIC_RELAXED);
+}
+
+// Exact single_flip_contiguous verdict on a grid: "(district a) minus v is connected".
+// The level-synchronous race search of fw_device.h (Ctx::race_search) and of the
+// oracle (contiguous_after), with visited marks in the shared 4-bit scratch (0 =
+// unvisited, 1+o = reached from source o, SCR_BLOCK = v) instead of in the labels.
+// Wave-cooperative: all 64 lanes call it for one chain; the caller holds the lock.
+template <int LB>
+__device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t* list,
+                          GLB uint32_t* spill, int qcap, int W, int H, uint64_t gmagic, int lane,
+                          int v, uint32_t a, int m, int src, uint64_t cls, uint64_t& bfs_nodes,
+                          uint64_t& bfs_deg) {
+  using P = PK<LB>;
+  using S = PK<4>;
+  auto list_get = [&](int i) -> uint32_t {
+    const uint32_t in_lds = list[i < qcap ? i : qcap - 1];
+    uint32_t in_hbm = 0;
+    if (i >= qcap) in_hbm = spill[i - qcap];
+    return i < qcap ? in_lds : in_hbm;
+  };
+  auto list_put = [&](int i, uint32_t x) {
+    if (i < qcap) list[i] = x;
+    if (i >= qcap) spill[i - qcap] = x;
+  };
+  if (lane == 0) S::axor(scr, v, SCR_BLOCK);
+  if (lane < m) {
+    S::axor(scr, src, 1u + (uint32_t)lane);
+    list_put(lane, (uint32_t)src);
+  }
+  lds_order();
+  int nl = m, lb = 0, le = m;
+  uint32_t my_deg = 0;
+  int verdict = -1;
+  for (;;) {
+    uint64_t rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
+    if (__popcll(rep) == 1) {
+      verdict = 1;
+      break;
+    }
+    uint64_t pushed_src = 0;
+    for (int base = lb; base < le; base += WAVE) {
+      const int idx = base + lane;
+      const bool act = idx < le;
+      const int x = act ? (int)list_get(idx) : 0;
+      const uint32_t o = act ? S::get(scr, x) - 1u : 0u;
+      const int xr = (int)(((uint64_t)(uint32_t)x * gmagic) >> 42);
+      const int xc = x - xr * W;
+      if (act) my_deg += (uint32_t)((xr > 0) + (xc > 0) + (xc < W - 1) + (xr < H - 1));
+      bfs_nodes += (uint64_t)__popcll(ballot(act));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int y = -1;
+        if (act) {
+          if (j == 0 && xr > 0) y = x - W;
+          if (j == 1 && xc > 0) y = x - 1;
+          if (j == 2 && xc < W - 1) y = x + 1;
+          if (j == 3 && xr < H - 1) y = x + W;
+        }
+        bool push = false, req = false;
+        uint32_t other = 0;
+        if (y >= 0 && P::get(lab, y) == a) {
+          const uint32_t got = S::claim(scr, y, 0u, 1u + o);
+          if (got == 0u) {
+            push = true;
+          } else if (got - 1u < (uint32_t)m) {  // v (SCR_BLOCK) is never a class
+            req = true;
+            other = got - 1u;
+          }
+        }
+        const uint64_t pm = ballot(push);
+        if (push) list_put(nl + (int)mbcnt(pm), (uint32_t)y);
+        nl += __popcll(pm);
+        if (pm) {
+          for (int si = 0; si < m; ++si)
+            pushed_src |= ballot(push && o == (uint32_t)si) ? (1ull << si) : 0ull;
+        }
+        uint64_t rm = ballot(req && o != other);
+        while (rm) {  // merges, serial over requesting lanes
+          const int Lr = __ffsll((unsigned long long)rm) - 1;
+          rm &= rm - 1;
+          const int o1 = rdl((int32_t)o, Lr), o2 = rdl((int32_t)other, Lr);
+          const uint64_t m1 = rdl64(cls, o1), m2 = rdl64(cls, o2);
+          if (m1 != m2) {
+            const uint64_t nm = m1 | m2;
+            if (lane < m && ((nm >> lane) & 1ull)) cls = nm;
+          }
+        }
+      }
+      if (nl > qcap) __threadfence_block();  // spilled entries are read next level
+    }
+    lds_order();
+    lb = le;
+    le = nl;
+    rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
+    if (__popcll(rep) == 1) {
+      verdict = 1;
+      break;
+    }
+    // a class with no pushes this level is closed: disconnected
+    const bool closed = lane < m && ((rep >> lane) & 1ull) && ((cls & pushed_src) == 0ull);
+    if (ballot(closed)) {
+      verdict = 0;
+      break;
+    }
+  }
+  bfs_deg += wave_sum(my_deg);
+  for (int base = 0; base < nl; base += WAVE) {  // clear the visited marks
+    const int idx = base + lane;
+    if (idx < nl) scr_clear(scr, (int)list_get(idx));
+  }
+  if (lane == 0) scr_clear(scr, v);
+  lds_order();
+  return verdict == 1;
+}
+
+template <int LB, int MODE, int PER>
+__global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
+  static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
   extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ int32_t s_lock;
+  using P = PK<LB>;
   const int lane = __lane_id(), row = lane >> 4, q = lane & 15;
+  const int wv = (int)(threadIdx.x >> 6);
   const int W = p.g.gw, H = p.g.gh, n = p.g.n, D = p.g.maxdeg, G = p.G, k = p.k;
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
-  LDS uint8_t* const lab = sm + row * p.slot_stride;  // this row's chain slot
-  LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);
+  LDS uint8_t* const lab = sm + (wv * 4 + row) * p.slot_stride;  // this row's chain slot
+  LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);  // u16 pairs
+  LDS uint8_t* const scr = sm + p.off_scr;                                        // shared
+  LDS uint32_t* const list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list16);  // shared
+  GLB uint32_t* const spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)n);
   const uint32_t key0 = (uint32_t)p.seed, key1 = (uint32_t)(p.seed >> 32);
-  using P = PK<4>;
+  const int GW = (G + 1) >> 1;  // u16-pair words of group sums
   int my_dr, my_dc;
   role_off(q <= 8 ? q : 0, my_dr, my_dc);
   auto divmod = [&](int x, int& r, int& c) {
     r = (int)(((uint64_t)(uint32_t)x * p.g.gmagic) >> 42);
     c = x - r * W;
   };
-  __shared__ int32_t s_base;
   STAMP_DECL
 
+  // the search scratch starts all-zero; every search clears what it marked
+  {
+    LDS uint32_t* s32 = reinterpret_cast<LDS uint32_t*>(scr);
+    for (int i = (int)threadIdx.x; i < p.scr_bytes / 4; i += (int)blockDim.x) s32[i] = 0u;
+    if (threadIdx.x == 0) s_lock = 0;
+  }
+  __syncthreads();
+
   for (;;) {
-    if (lane == 0) s_base = atomicAdd(p.next_chain, 4);
-    __syncthreads();
-    const int cbase = rfl(s_base);
+    int cb = 0;
+    if (lane == 0) cb = atomicAdd(p.next_chain, 4);
+    const int cbase = rdl(cb, 0);
     if (cbase >= p.n_chains) break;
     const int c = cbase + row;
     const bool has = c < p.n_chains;
@@ -180,22 +317,26 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0, n_sdeg = 0, n_adeg = 0, n_bchg = 0;
     uint32_t n_yield = 0, retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
-    __syncthreads();
+    lds_order();
 
     // ---- derive group sums, cut / boundary / proposal-set counts (per row)
     int32_t cut, bnodes, npairs;
     {
       uint32_t cut2 = 0, bn = 0, np = 0;
-      for (int t = 0; t < G; ++t) {
-        uint32_t w4, cd4;
-        weights4<MODE>(lab, t * 64 + q * 4, W, H, n, p.g.gmagic, w4, cd4);
-        const uint32_t ws = bsum4(w4);
-        cut2 += bsum4(cd4);
-        bn += ((cd4 & 0xFFu) != 0) + ((cd4 & 0xFF00u) != 0) + ((cd4 & 0xFF0000u) != 0) +
-              ((cd4 & 0xFF000000u) != 0);
-        np += ws;
-        const uint32_t tot = row_sum(ws);
-        if (q == 0 && has) gsum[t] = tot;
+      for (int t2 = 0; t2 < GW; ++t2) {
+        uint32_t tot[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t w4, cd4;
+          weights4<LB, MODE>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, p.g.gmagic, w4, cd4);
+          const uint32_t ws = bsum4(w4);
+          cut2 += bsum4(cd4);
+          bn += ((cd4 & 0xFFu) != 0) + ((cd4 & 0xFF00u) != 0) + ((cd4 & 0xFF0000u) != 0) +
+                ((cd4 & 0xFF000000u) != 0);
+          np += ws;
+          tot[h] = row_sum(ws);
+        }
+        if (q == 0 && has) gsum[t2] = tot[0] | (tot[1] << 16);
       }
       cut = (int32_t)(row_sum(cut2) / 2);
       bnodes = (int32_t)row_sum(bn);
@@ -256,24 +397,26 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
                     key1);
         bpos = 0;
       }
-      const int src = (row * ROW + bpos) * 4;  // ds_bpermute byte address of the source lane
-      const U4 x = {(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x0),
-                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x1),
-                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x2),
-                    (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb.x3)};
+      const int srcl = (row * ROW + bpos) * 4;  // ds_bpermute byte address of the source lane
+      const U4 x = {(uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x0),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x1),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x2),
+                    (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x3)};
       ++bpos;
       attempts += act ? 1u : 0u;
       const uint32_t r = scale64(x.x0, x.x1, (uint32_t)(npairs > 0 ? npairs : 1));
 
       STAMP(0);  // draw
-      // ---- select, level 1: group sums (PER per lane)
+      // ---- select, level 1: group sums (PER per lane, read as PER/2 u16 pairs)
       uint32_t gs[PER];
       uint32_t s = 0;
 #pragma unroll
-      for (int t = 0; t < PER; ++t) {
-        const int gi = q * PER + t;
-        gs[t] = gi < G ? gsum[gi] : 0u;
-        s += gs[t];
+      for (int t = 0; t < PER / 2; ++t) {
+        const int wi = q * (PER / 2) + t;
+        const uint32_t w2 = wi < GW ? gsum[wi] : 0u;
+        gs[2 * t] = w2 & 0xFFFFu;
+        gs[2 * t + 1] = w2 >> 16;
+        s += gs[2 * t] + gs[2 * t + 1];
       }
       const uint32_t incl = row_scan(s);
       const uint32_t rb1 = rowbits(ballot(incl > r), row);
@@ -300,7 +443,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
-      weights4<MODE>(lab, x0, W, H, n, p.g.gmagic, w4, cd4);
+      weights4<LB, MODE>(lab, x0, W, H, n, p.g.gmagic, w4, cd4);
       const uint32_t ws = bsum4(w4);
       const uint32_t incl2 = row_scan(ws);
       const uint32_t rb2 = rowbits(ballot(incl2 > r1), row);
@@ -396,7 +539,7 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
       const bool pop_ok = rowbits(ballot(bad), row) == 0u;
 
       STAMP(3);  // gather, target, Δcut, population
-      // ---- contiguity: 8-cell ring test, exact race search when inconclusive
+      // ---- contiguity: 8-cell ring test, 7x7 window, exact race search when undecided
       const uint32_t rbits8 = rowbits(ballot(q >= 1 && q <= 8 && h.lx == a), row) >> 1;
       const int pN = rbits8 & 1, pW = (rbits8 >> 1) & 1, pE = (rbits8 >> 2) & 1, pS = (rbits8 >> 3) & 1;
       const int NE = (rbits8 >> 4) & 1, SE = (rbits8 >> 5) & 1, SW = (rbits8 >> 6) & 1,
@@ -409,43 +552,47 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
           const int pos = window_pos(q + ROW * t);
-          const int rr = vr - 3 + pos / 7, cc = vc - 3 + pos % 7;
-          const bool in = rr >= 0 && rr < H && cc >= 0 && cc < W && P::get(lab, rr * W + cc) == a;
+          const int rr = vr - 3 + pos / 7, cw = vc - 3 + pos % 7;
+          const bool in = rr >= 0 && rr < H && cw >= 0 && cw < W && P::get(lab, rr * W + cw) == a;
           A |= (uint64_t)rowbits(ballot(in), row) << (ROW * t);
         }
         A = (A & ((1ull << 24) - 1ull)) | ((A >> 24) << 25);
-        const int wv = need ? window_verdict(A) : -1;
-        if (wv >= 0) {
-          contig = wv == 1;
+        const int wvd = need ? window_verdict(A) : -1;
+        if (wvd >= 0) {
+          contig = wvd == 1;
           need = false;
         }
       }
       uint64_t rows_need = ballot(q == 0 && need);
+      if (rows_need) {
+        // the scratch and visit list are shared by the workgroup's waves
+        if (lane == 0) {
+          int expect = 0;
+          while (!__hip_atomic_compare_exchange_strong(&s_lock, &expect, 1, __ATOMIC_ACQUIRE,
+                                                       __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            expect = 0;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        lds_order();
+      }
       while (rows_need) {  // wave-cooperative exact search, one chain slot at a time
         const int L0 = __ffsll((unsigned long long)rows_need) - 1;
         rows_need &= rows_need - 1;
         const int rr = L0 >> 4;
-        Ctx<4, true> C;
-        C.g = p.g;
-        C.lab = sm + rr * p.slot_stride;
-        C.gsum = nullptr;
-        C.list = reinterpret_cast<LDS uint32_t*>(sm + 4 * p.slot_stride);  // shared list
-        C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)n);
-        C.qcap = p.qcap;
-        C.k = k;
-        C.lane = lane;
         const int vv = rdl(v, L0);
         const uint32_t aa = rdl(a, L0);
         const uint32_t am4 = rdl(amb, L0);
         const int mr = __popc(am4);
         // sources in CSR order (up, left, right, down) into lanes 0..m-1
-        int src = -1;
+        int srcn = -1;
         uint32_t mm = am4;
         for (int i = 0; i < mr; ++i) {
           const int bit = __ffs(mm) - 1;
           mm &= mm - 1;
           const int val = rdl(h.x, L0 + 1 + bit);
-          if (lane == i) src = val;
+          if (lane == i) srcn = val;
         }
         uint64_t cls = lane < mr ? (1ull << lane) : 0ull;
         const uint32_t lk = rdl((uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)), L0);
@@ -459,13 +606,17 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
         if (lk & 4) merge(sx(3), sx(1));  // S-W
         if (lk & 8) merge(sx(1), sx(0));  // W-N
         uint64_t bn = 0, bd = 0;
-        const bool ok = C.race_search(vv, aa, mr, src, cls, bn, bd);
+        const bool ok = grid_race<LB>(sm + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
+                                      p.qcap16, W, H, p.g.gmagic, lane, vv, aa, mr, srcn, cls, bn,
+                                      bd);
         if (row == rr) {
           contig = ok;
           n_bfs += 1;
           n_bfsn += bn;
           n_bfsd += bd;
         }
+        if (rows_need == 0 && lane == 0)
+          __hip_atomic_store(&s_lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
 
       STAMP(4);  // ring test + exact searches
@@ -507,7 +658,10 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
       }
       if (accepted) {
         if (q == 0) P::axor(lab, v, a ^ d);
-        if (mine && wn != wo) lds_add(gsum + (h.x >> 6), wn - wo);
+        // u16 group sum inside its u32 pair: a wrapping 32-bit add of the shifted
+        // delta changes only that half (both halves stay in [0, 65535])
+        if (mine && wn != wo)
+          lds_add(gsum + (h.x >> 7), (wn - wo) << (16 * ((h.x >> 6) & 1)));
       }
       lds_order();
       const uint64_t b_plus = ballot(accepted && mine && wo == 0 && wn > 0);
@@ -562,18 +716,20 @@ __global__ __launch_bounds__(64) void fw_grid16_kernel(FwRunParams p) {
         stp->stuck = stuck;
       }
     }
-    __syncthreads();
+    lds_order();
   }
   STAMP_FLUSH
 }
 
-template <int MODE>
+template <int LB, int MODE>
 void* pick16(int G) {
-  if (G <= 16 * 2) return reinterpret_cast<void*>(&fw_grid16_kernel<MODE, 2>);
-  if (G <= 16 * 4) return reinterpret_cast<void*>(&fw_grid16_kernel<MODE, 4>);
-  if (G <= 16 * 10) return reinterpret_cast<void*>(&fw_grid16_kernel<MODE, 10>);
-  return reinterpret_cast<void*>(&fw_grid16_kernel<MODE, 16>);
+  if (G <= 16 * 2) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2>);
+  if (G <= 16 * 4) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4>);
+  if (G <= 16 * 10) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10>);
+  return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16>);
 }
+
+int round16i(int x) { return (x + 15) / 16 * 16; }
 
 }  // namespace
 
@@ -589,11 +745,66 @@ extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-bool fw_grid16_supported(const FwRunParams& p, int lb) {
-  return p.g.gw > 0 && lb == 4 && p.G <= 16 * 16 && p.k <= 15 && p.g.maxdeg == 4;
+bool fw_grid16_candidate(int gw, int maxdeg, int G, int k) {
+  return gw > 0 && maxdeg == 4 && G <= 16 * 16 && k <= 15;
 }
 
 void* fw_grid16_fn(const FwRunParams& p) {
-  return p.mode == FW_PROPOSE_CUTEDGE ? pick16<FW_PROPOSE_CUTEDGE>(p.G)
-                                      : pick16<FW_PROPOSE_PAIRS>(p.G);
+  const bool cut = p.mode == FW_PROPOSE_CUTEDGE;
+  if (p.lb == 2)
+    return cut ? pick16<2, FW_PROPOSE_CUTEDGE>(p.G) : pick16<2, FW_PROPOSE_PAIRS>(p.G);
+  return cut ? pick16<4, FW_PROPOSE_CUTEDGE>(p.G) : pick16<4, FW_PROPOSE_PAIRS>(p.G);
+}
+
+// LDS plan of the grid kernel: per chain slot [labels | u16 group sums], slot stride
+// 16 B mod 128 B so the four rows of a wave start on different banks; then the shared
+// 4-bit search scratch and visit list.  Picks the waves per workgroup (1..4) that keep
+// the most chains resident per CU (ties: fewer waves).
+int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
+  const int slot = round16i(p.lab_bytes + 4 * ((p.G + 1) / 2));
+  int stride = slot;
+  while (stride % 128 != 16) stride += 16;
+  p.slot_stride = stride;
+  p.off_gsum = round16i(p.lab_bytes);
+  p.scr_bytes = round16i((p.g.n + 1) / 2 + 8);
+  if (p.qcap16 <= 0) p.qcap16 = 384;
+  void* fn = fw_grid16_fn(p);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
+  int best_nw = 0, best_chains = 0, best_lds = 0;
+  for (int nw = 1; nw <= MAX_NW; ++nw) {
+    const int lds = 4 * nw * stride + p.scr_bytes + 4 * p.qcap16;
+    if (lds > 160 * 1024 - 256) break;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+      return -1;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nw, (size_t)lds) !=
+        hipSuccess)
+      return -1;
+    if (per_cu * 4 * nw > best_chains) {
+      best_chains = per_cu * 4 * nw;
+      best_nw = nw;
+      best_lds = lds;
+    }
+  }
+  if (best_nw == 0) return -1;
+  p.nw = best_nw;
+  p.off_scr = 4 * best_nw * stride;
+  p.off_list16 = p.off_scr + p.scr_bytes;
+  p.lds16 = best_lds;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, best_lds) != hipSuccess)
+    return -1;
+  const long long per_wg = 4LL * best_nw;
+  long long gsz = (long long)(best_chains / per_wg) * prop.multiProcessorCount;
+  const long long need = (p.n_chains + per_wg - 1) / per_wg;
+  if (gsz > need) gsz = need;
+  *grid = (int)(gsz < 1 ? 1 : gsz);
+  return 0;
+}
+
+int fw_grid16_launch(const FwRunParams& p, int grid, void* stream) {
+  void* args[] = {const_cast<FwRunParams*>(&p)};
+  hipError_t e = hipLaunchKernel(fw_grid16_fn(p), dim3(grid), dim3(64 * p.nw), args,
+                                 (size_t)p.lds16, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : -1;
 }

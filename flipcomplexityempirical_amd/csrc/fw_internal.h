@@ -44,8 +44,14 @@ struct FwRunParams {
   // LDS layout (bytes from the dynamic shared base)
   int32_t lab_bytes;           // packed label bytes (multiple of 16)
   int32_t off_gsum, off_list, lds_bytes;
-  int32_t slot_stride;         // grid16 kernel: bytes between the four chain slots
+  int32_t lb;                  // label bits per node (2, 4 or 8)
   int32_t use16;               // 1: launch the four-chains-per-wave grid kernel
+  // grid kernel LDS plan (fw_grid16_plan): 4*nw chain slots, shared scratch and list
+  int32_t slot_stride;         // bytes between chain slots
+  int32_t nw;                  // waves per workgroup
+  int32_t off_scr, scr_bytes;  // 4-bit search scratch
+  int32_t off_list16, qcap16;  // shared visit list
+  int32_t lds16;               // dynamic LDS bytes per workgroup
 };
 
 struct FwEvalParams {
@@ -71,5 +77,7 @@ int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);
 // fw_grid16.hip
-bool fw_grid16_supported(const FwRunParams& p, int lb);
+bool fw_grid16_candidate(int gw, int maxdeg, int G, int k);
 void* fw_grid16_fn(const FwRunParams& p);
+int fw_grid16_plan(FwRunParams& p, int device, int* grid);
+int fw_grid16_launch(const FwRunParams& p, int grid, void* stream);

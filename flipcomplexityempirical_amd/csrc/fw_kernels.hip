@@ -24,8 +24,6 @@
 // bit for bit (tests/test_gpu_parity.py).
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
 #include "fw_device.h"
 
 namespace {
@@ -329,37 +327,28 @@ void* pick_run(int lb, bool grid, int mode, int G) {
 
 }  // namespace
 
+// Occupancy-sized persistent grid for the one-chain-per-wave kernel.
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   if (p.G > 64 * 16) return -2;
-  const char* no16 = getenv("FLIPWALK_NO_GRID16");  // A/B switch: one chain per wave
-  p.use16 = fw_grid16_supported(p, lb) && !(no16 && no16[0] == '1') ? 1 : 0;
-  // grid16: four chain slots (labels | group sums) per workgroup, strides offset by
-  // 16 B mod 128 B (banks), then ONE search list shared by the four chains (the exact
-  // search runs for one chain at a time)
-  p.slot_stride = (p.off_list + 127) / 128 * 128 + 16;
-  if (p.use16) p.qcap = 768;  // 3 KB shared list: 6 workgroups (24 chains) per CU at 100x100
-  void* fn = p.use16 ? fw_grid16_fn(p) : pick_run(lb, p.g.gw > 0, p.mode, p.G);
-  const int lds = p.use16 ? 4 * p.slot_stride + p.qcap * 4 : p.lds_bytes;
-  const int chains_per_wg = p.use16 ? 4 : 1;
-  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  void* fn = pick_run(lb, p.g.gw > 0, p.mode, p.G);
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   if (e != hipSuccess) return -1;
   int per_cu = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, (size_t)lds);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, (size_t)p.lds_bytes);
   if (e != hipSuccess || per_cu <= 0) return -1;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
   long long gsz = (long long)per_cu * prop.multiProcessorCount;
-  const long long need = (p.n_chains + chains_per_wg - 1) / chains_per_wg;
-  if (gsz > need) gsz = need;
+  if (gsz > p.n_chains) gsz = p.n_chains;
   *grid = (int)(gsz < 1 ? 1 : gsz);
   return 0;
 }
 
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
-  void* fn = p.use16 ? fw_grid16_fn(p) : pick_run(lb, p.g.gw > 0, p.mode, p.G);
-  const int lds = p.use16 ? 4 * p.slot_stride + p.qcap * 4 : p.lds_bytes;
+  if (p.use16) return fw_grid16_launch(p, grid, stream);
+  void* fn = pick_run(lb, p.g.gw > 0, p.mode, p.G);
   void* args[] = {const_cast<FwRunParams*>(&p)};
-  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)lds, (hipStream_t)stream);
+  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes, (hipStream_t)stream);
   return e == hipSuccess ? 0 : -1;
 }
 

@@ -130,3 +130,43 @@ def test_stuck_flag_instead_of_hang(gpu_lib):
     st = ch.stats()
     assert st["stuck"].all() and (st["steps"] == 0).all() and (st["attempts"] == 50).all()
     assert (ch.labels() == lab).all()
+
+
+def _run_vs_oracle(case, n_chains, steps_list, seed=99, id0=3):
+    dg = DeviceGraph(case.graph)
+    ch = Chains(dg, n_chains, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                base=case.base, seed=seed, chain_id0=id0)
+    for s in steps_list:
+        ch.run(s)
+    labs, st, pops = ch.labels(), ch.stats(), ch.pops()
+    olabs, ost, opops, ohc, ohb = oracle_chains(case, seed, range(id0, id0 + n_chains), steps_list)
+    assert np.array_equal(labs, olabs)
+    assert_stats_equal(st, ost)
+    assert np.array_equal(pops, opops)
+    assert np.array_equal(ch.hist_cut(), ohc)
+    assert np.array_equal(ch.hist_b(), ohb)
+    return st
+
+
+@pytest.mark.parametrize("name", ["grid20_k4_mu", "grid16x24_k8", "grid30x18_k2_bi"])
+def test_many_chains_per_workgroup(gpu_lib, name, monkeypatch):
+    """77 chains: several waves and workgroups, contended search lock, a ragged last wave."""
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    st = _run_vs_oracle(case, 77, [300, 500])
+    assert st["bfs_runs"].sum() > 0
+
+
+@pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
+                                       ("grid30x18_k2_bi", "auto"), ("sec11_a2_k2", "auto"),
+                                       ("tract_k4", "auto")])
+def test_search_list_spill(gpu_lib, name, path, monkeypatch):
+    """A 2-entry LDS visit list: every exact search spills to its HBM slice."""
+    monkeypatch.setenv("FLIPWALK_LIST_CAP", "2")
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    st = _run_vs_oracle(case, 21, [400, 400])
+    assert (st["bfs_nodes"] > 2 * st["bfs_runs"]).any()  # searches did outgrow the LDS list
