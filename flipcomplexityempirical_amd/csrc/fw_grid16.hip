@@ -139,6 +139,88 @@ __device__ __forceinline__ uint32_t bsum4(uint32_t v) {
   return (v & 0xFFu) + ((v >> 8) & 0xFFu) + ((v >> 16) & 0xFFu) + (v >> 24);
 }
 
+// ---- SWAR form for 2-bit labels (k <= 4): the four nodes of a lane are the four bytes
+// of a dword.  A label becomes a one-hot byte (1 << label) with one v_perm_b32, so a
+// node's neighbour label set is an OR of bytes and its weight a per-byte popcount.
+__device__ __forceinline__ uint32_t spread4(uint32_t u) {  // fields 0..3 of u (2 bits) -> bytes
+  const uint32_t t = ((u << 12) | u) & 0x000F000Fu;
+  return ((t << 6) | t) & 0x03030303u;
+}
+__device__ __forceinline__ uint32_t onehot4(uint32_t s) {  // bytes 0..3 -> 1 << byte
+  return __builtin_amdgcn_perm(0u, 0x08040201u, s);
+}
+__device__ __forceinline__ uint32_t low_bytes(int t) {  // 0xFF in bytes 0..t-1
+  return t >= 4 ? 0xFFFFFFFFu : (t <= 0 ? 0u : (1u << (8 * t)) - 1u);
+}
+__device__ __forceinline__ uint32_t byte_clear(int t) {  // all bytes but byte t (t in 0..3)
+  return t >= 0 && t < 4 ? ~(0xFFu << (8 * t)) : 0xFFFFFFFFu;
+}
+// per byte: 0x80 where the one-hot bytes a and b differ (different labels)
+__device__ __forceinline__ uint32_t ne_bytes(uint32_t a, uint32_t b) {
+  return ~((a & b) + 0x7F7F7F7Fu) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t byte_popc(uint32_t f) {  // per-byte popcount (bytes < 16)
+  const uint32_t t = f - ((f >> 1) & 0x55555555u);
+  return (t & 0x33333333u) + ((t >> 2) & 0x33333333u);
+}
+
+template <int MODE, bool NEED_CD>
+__device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, int W, int H, int n,
+                                              uint64_t gmagic, uint32_t& w4, uint32_t& cd4) {
+  w4 = 0;
+  cd4 = 0;
+  if (x0 >= n) return;
+  const uint32_t own = lab_window<2>(lab, x0);  // fields x0-1 .. x0+4
+  const uint32_t up = x0 + 3 - W >= 0 ? lab_window<2>(lab, x0 - W) : 0u;
+  const uint32_t dn = x0 + W < n ? lab_window<2>(lab, x0 + W) : 0u;
+  const uint32_t o_lo = onehot4(spread4(own)), o_hi = onehot4(spread4(own >> 8));
+  const uint32_t L = o_lo;                                     // x-1
+  const uint32_t O = __builtin_amdgcn_alignbyte(o_hi, o_lo, 1);  // x
+  const uint32_t R = __builtin_amdgcn_alignbyte(o_hi, o_lo, 2);  // x+1
+  const uint32_t U = onehot4(spread4(up >> 2)), Dn = onehot4(spread4(dn >> 2));
+  // which of the four nodes have each neighbour (W >= 4: at most one row wrap, at tw)
+  const int r0 = (int)(((uint64_t)(uint32_t)x0 * gmagic) >> 42);
+  const int c0 = x0 - r0 * W;
+  const int tw = W - c0;  // first byte on the next grid row (>= 4: none)
+  const uint32_t mN = low_bytes(n - x0);
+  const uint32_t mU = r0 == 0 ? ~low_bytes(tw) : 0xFFFFFFFFu;
+  const uint32_t mD = r0 == H - 1 ? low_bytes(tw) ^ 0xFFFFFFFFu
+                                  : (r0 + 1 == H - 1 ? low_bytes(tw) : 0xFFFFFFFFu);
+  const uint32_t mL = byte_clear(c0 == 0 ? 0 : tw);
+  const uint32_t mR = byte_clear(tw - 1);
+  if constexpr (MODE != FW_PROPOSE_CUTEDGE) {
+    const uint32_t bits = (U & mU) | (L & mL) | (R & mR) | (Dn & mD);
+    w4 = byte_popc(bits & ~O & mN);
+  }
+  if constexpr (NEED_CD || MODE == FW_PROPOSE_CUTEDGE) {
+    const uint32_t ne = (ne_bytes(U, O) & mU) >> 7, nl = (ne_bytes(L, O) & mL) >> 7,
+                   nr = (ne_bytes(R, O) & mR) >> 7, nd = (ne_bytes(Dn, O) & mD) >> 7;
+    cd4 = (ne + nl + nr + nd) & mN;
+    if constexpr (MODE == FW_PROPOSE_CUTEDGE) w4 = cd4;
+  }
+}
+
+// weights (and, when NEED_CD, cut degrees) of nodes x0..x0+3, one per byte
+template <int LB, int MODE, bool NEED_CD>
+__device__ __forceinline__ void weights4x(const LDS uint8_t* lab, int x0, int W, int H, int n,
+                                          uint64_t gmagic, uint32_t& w4, uint32_t& cd4) {
+  if constexpr (LB == 2)
+    weights4_swar<MODE, NEED_CD>(lab, x0, W, H, n, gmagic, w4, cd4);
+  else
+    weights4<LB, MODE>(lab, x0, W, H, n, gmagic, w4, cd4);
+}
+
+// bytes of w (each < 64) summed
+__device__ __forceinline__ uint32_t bsum4m(uint32_t v) { return (v * 0x01010101u) >> 24; }
+
+// Launders a wave-uniform value into a VGPR (keeps it out of the scarce SGPRs; the
+// volatile asm is not hoisted, so per-use copies are not turned back into SGPR constants)
+__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+
 // 4-bit scratch field x := 0 (atomic on the shared word)
 __device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
   __atomic_fetch_and(PK<4>::word(scr, x), ~(15u << PK<4>::shift(x)), __ATOMIC_RELAXED);
@@ -328,9 +410,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           uint32_t w4, cd4;
-          weights4<LB, MODE>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, p.g.gmagic, w4, cd4);
-          const uint32_t ws = bsum4(w4);
-          cut2 += bsum4(cd4);
+          weights4x<LB, MODE, true>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, p.g.gmagic, w4, cd4);
+          const uint32_t ws = bsum4m(w4);
+          cut2 += bsum4m(cd4);
           bn += ((cd4 & 0xFFu) != 0) + ((cd4 & 0xFF00u) != 0) + ((cd4 & 0xFF0000u) != 0) +
                 ((cd4 & 0xFF000000u) != 0);
           np += ws;
@@ -393,8 +475,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 
       if (bpos == ROW) {
         const uint64_t t = attempts + (uint64_t)q;
-        pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32), key0,
-                    key1);
+        pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
+                    in_vgpr(key0), in_vgpr(key1));
         bpos = 0;
       }
       const int srcl = (row * ROW + bpos) * 4;  // ds_bpermute byte address of the source lane
@@ -443,24 +525,17 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
-      weights4<LB, MODE>(lab, x0, W, H, n, p.g.gmagic, w4, cd4);
-      const uint32_t ws = bsum4(w4);
+      weights4x<LB, MODE, false>(lab, x0, W, H, n, p.g.gmagic, w4, cd4);
+      const uint32_t pref = w4 * 0x01010101u;  // byte t: weights of nodes 0..t (<= 16)
+      const uint32_t ws = pref >> 24;
       const uint32_t incl2 = row_scan(ws);
       const uint32_t rb2 = rowbits(ballot(incl2 > r1), row);
       const int L2 = __ffs(rb2) - 1;
-      uint32_t r2 = r1 - (incl2 - ws), c3 = 0, bef2 = 0;
-      int t2 = 3;
-      bool f2 = false;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const uint32_t c4 = c3 + ((w4 >> (8 * tt)) & 0xFFu);
-        if (!f2 && r2 < c4) {
-          t2 = tt;
-          bef2 = c3;
-          f2 = true;
-        }
-        c3 = c4;
-      }
+      const uint32_t r2 = min(r1 - (incl2 - ws), 127u);  // < ws on the chosen lane
+      // first byte with prefix > r2 (SWAR compare; no borrow across bytes as r2 < 128)
+      const uint32_t gt = ((pref | 0x80808080u) - (r2 + 1u) * 0x01010101u) & 0x80808080u;
+      const int t2 = gt ? (__ffs(gt) - 1) >> 3 : 3;
+      const uint32_t bef2 = t2 ? (pref >> (8 * t2 - 8)) & 0xFFu : 0u;
       const uint32_t pk2 = row_pick(((uint32_t)(q * 4 + t2) << 16) | ((r2 - bef2) & 0xFFFFu), L2, q);
       const int v = min(gi * 64 + (int)(pk2 >> 16), n - 1);
       const uint32_t j = pk2 & 0xFFFFu;
@@ -746,7 +821,8 @@ extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 bool fw_grid16_candidate(int gw, int maxdeg, int G, int k) {
-  return gw > 0 && maxdeg == 4 && G <= 16 * 16 && k <= 15;
+  // gw >= 4: four consecutive nodes span at most one row wrap (weights4_swar masks)
+  return gw >= 4 && maxdeg == 4 && G <= 16 * 16 && k <= 15;
 }
 
 void* fw_grid16_fn(const FwRunParams& p) {
