@@ -10,6 +10,11 @@ Replaces the networkx / ``gerrychain.Graph`` objects the reference builds:
 * ``Graph.from_json(path)`` — ``gerrychain.Graph.from_json`` (All_States_Chain.py:208,221),
   networkx adjacency-JSON, including the TOTPOP str->int cast (All_States_Chain.py:227-230).
 * ``Graph.from_networkx(G)``.
+* ``frankenstein_graph()`` — the "Frankengraph" of Frankenstein_chain.py:188-197 /
+  construct_FRANK.py: a 50x50 square grid glued along one row to a triangular lattice
+  (5,000 nodes, 12,300 edges, max degree 6), with the three seed plans of :209-248.
+* ``delaunay_graph()``      — the C4 benchmark graph: Delaunay triangulation
+  of 9,000 uniform points, lognormal integer populations (a VTD-style dual graph).
 
 Canonical form (what every other component assumes): node ids 0..n-1 in sorted order
 of the original node keys, neighbour lists strictly ascending, no self loops,
@@ -237,3 +242,72 @@ def band_seed(h: int, w: int, k: int) -> np.ndarray:
 def stripe_seed(h: int, w: int) -> np.ndarray:
     """Rows i >= h/2 -> 1, else 0 (the sec11 'alignment 0' analogue used for C1)."""
     return (np.arange(h)[:, None] >= h // 2).repeat(w, axis=1).astype(np.int16).reshape(-1)
+
+
+# ---------------------------------------------------------------- Frankengraph
+def frankenstein_graph(m: int = 50) -> Graph:
+    """Frankenstein_chain.py:188-197: nx.compose(relabelled m x m grid, triangular lattice).
+
+    Node keys are the reference's (x, y) tuples; node attributes carry ``boundary_node``
+    (:259-265: x == 0, x == m-1, y == m or y == -m+1) for the boundary_condition rule.
+    """
+    import networkx as nx
+    G = nx.grid_graph([m, m])
+    H = nx.triangular_lattice_graph(m, 2 * m - 2)
+    G = nx.relabel_nodes(G, {x: (x[0], x[1] - m + 1) for x in G.nodes()})
+    F = nx.compose(G, H)
+    nodes = list(F.nodes())
+    adj = {x: list(F.neighbors(x)) for x in nodes}
+    attrs = [{"population": 1,
+              "boundary_node": bool(x[0] == 0 or x[0] == m - 1 or x[1] == m or x[1] == -m + 1)}
+             for x in nodes]
+    return Graph.from_adjacency(nodes, adj, None, attrs)
+
+
+def frankenstein_seed(g: Graph, alignment: int, m: int = 50) -> np.ndarray:
+    """Seed plans of Frankenstein_chain.py:209-248 (start_plans = [diagonal, vertical,
+    horizontal]; members -> 1, others -> -1), labels {-1, 1} mapped to {0, 1}."""
+    lab = np.zeros(g.n, np.int16)
+    for i, (x, y) in enumerate(g.nodes):
+        if alignment == 0:
+            inside = 2 * x - y <= m - 3
+        elif alignment == 1:
+            inside = x < m / 2
+        elif alignment == 2:
+            inside = y < 0
+        else:
+            raise ValueError("alignment must be 0, 1 or 2")
+        lab[i] = 1 if inside else 0
+    return lab
+
+
+def boundary_flags(g: Graph) -> np.ndarray:
+    """uint8 per node: the ``boundary_node`` attribute (grid_chain_sec11.py:225-233 marks
+    the outer ring of the grid; Frankenstein_chain.py:259-265 the Frankengraph rim)."""
+    if g.node_attrs is not None and g.node_attrs and "boundary_node" in g.node_attrs[0]:
+        return np.array([1 if a["boundary_node"] else 0 for a in g.node_attrs], np.uint8)
+    if g.nodes and isinstance(g.nodes[0], tuple):
+        xs = np.array([k[0] for k in g.nodes])
+        ys = np.array([k[1] for k in g.nodes])
+        return ((xs == xs.min()) | (xs == xs.max()) | (ys == ys.min()) |
+                (ys == ys.max())).astype(np.uint8)
+    raise ValueError("graph has no boundary_node attribute and no coordinate keys")
+
+
+# ---------------------------------------------------------------- C4 dual graph
+def delaunay_graph(n_points: int = 9000, seed: int = 0, pop_median: float = 1000.0,
+                   pop_sigma: float = 0.8) -> Graph:
+    """Delaunay triangulation of ``n_points`` points drawn by
+    ``np.random.default_rng(seed).random((n, 2))``, node populations
+    ``max(1, round(lognormal(ln pop_median, pop_sigma)))`` from the same generator."""
+    from scipy.spatial import Delaunay
+    rng = np.random.default_rng(seed)
+    pts = rng.random((n_points, 2))
+    tri = Delaunay(pts)
+    indptr, indices = tri.vertex_neighbor_vertices
+    pop = np.maximum(1, np.rint(rng.lognormal(np.log(pop_median), pop_sigma, n_points))).astype(
+        np.int64)
+    nodes = list(range(n_points))
+    adj = {v: indices[indptr[v]:indptr[v + 1]].tolist() for v in nodes}
+    attrs = [{"x": float(pts[v, 0]), "y": float(pts[v, 1])} for v in nodes]
+    return Graph.from_adjacency(nodes, adj, pop.tolist(), attrs)

@@ -6,7 +6,9 @@ reference calls as ``recursive_tree_part(graph, [-1, 1], totpop/2, "TOTPOP", .05
 spanning tree (minimum spanning tree under i.i.d. uniform edge weights), rooting it,
 and cutting a uniformly chosen tree edge whose side has population within
 ``epsilon * pop_target`` of ``pop_target``; redraw the tree when no edge qualifies.
-The last district takes the remainder.  GerryChain is not installed, so the draw
+The last district takes the remainder.  As in GerryChain 0.2.x's recursive_tree_part, a
+running population "debt" narrows each split's window so that the remainder, too, ends
+within ``epsilon`` of ``pop_target``.  GerryChain is not installed, so the draw
 sequence is our own (numpy ``default_rng``); the law over plans follows the
 published algorithm.  Grid seeds (grid_chain_sec11.py:194-214) live in ``graph``.
 """
@@ -83,8 +85,14 @@ def recursive_tree_part(graph: Graph, parts: Sequence, pop_target: float, epsilo
     pop = graph.pop_array()
     remaining = np.arange(graph.n)
     lab = np.full(graph.n, len(parts) - 1, np.int16)
+    debt = 0.0
     for i in range(len(parts) - 1):
-        subset = _balanced_cut(graph.rowptr, graph.col, pop, remaining, pop_target, epsilon, rng)
+        min_pop = max(pop_target * (1 - epsilon), pop_target * (1 - epsilon) - debt)
+        max_pop = min(pop_target * (1 + epsilon), pop_target * (1 + epsilon) - debt)
+        target = (min_pop + max_pop) / 2
+        subset = _balanced_cut(graph.rowptr, graph.col, pop, remaining, target,
+                               (max_pop - min_pop) / (2 * target), rng)
         lab[subset] = i
+        debt += float(pop[subset].sum()) - pop_target
         remaining = np.setdiff1d(remaining, subset)
     return lab

@@ -15,8 +15,10 @@ from typing import Optional
 import numpy as np
 
 from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
-from flipcomplexityempirical_amd.graph import (Graph, band_seed, block_seed, grid_graph,
+from flipcomplexityempirical_amd.graph import (Graph, band_seed, block_seed, delaunay_graph,
+                                               frankenstein_graph, frankenstein_seed, grid_graph,
                                                sec11_graph, sec11_seed, stripe_seed)
+from flipcomplexityempirical_amd.seeds import recursive_tree_part
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 MU = 2.63815853
@@ -53,6 +55,17 @@ class Case:
         return metropolis_table(self.base, self.graph.maxdeg)
 
 
+def c4_seed(g: Graph, k: int, percent: float = 0.05) -> np.ndarray:
+    """recursive_tree_part seed (All_States_Chain.py:232) valid for the chain's bounds."""
+    from oracle import oracle as O
+    lo, hi = population_bounds(g.total_pop, k, percent)
+    for s in range(50):
+        lab = recursive_tree_part(g, list(range(k)), g.total_pop / k, percent, seed=s)
+        if O.plan_valid(g, lab, k, lo, hi):
+            return lab
+    raise RuntimeError("no valid tree seed")
+
+
 def cases(include_kansas: bool = True):
     out = [
         Case("grid10_k2_bi", grid_graph(10, 10), stripe_seed(10, 10), 2, 0, 0.10, MU),
@@ -68,6 +81,11 @@ def cases(include_kansas: bool = True):
     g11 = sec11_graph()
     out.append(Case("sec11_a2_k2", g11, sec11_seed(g11, 2), 2, 0, 0.05, 0.1))
     out.append(Case("sec11_a0_k2_mu", g11, sec11_seed(g11, 0), 2, 0, 0.10, MU))
+    gf = frankenstein_graph()
+    out.append(Case("frank_a2_k2", gf, frankenstein_seed(gf, 2), 2, 0, 0.5, 1 / .379))
+    out.append(Case("frank_a0_k2_cold", gf, frankenstein_seed(gf, 0), 2, 0, 0.1, 0.3))
+    gd = delaunay_graph(3000, seed=1)
+    out.append(Case("delaunay3k_k18", gd, c4_seed(gd, 18), 18, 1, 0.05, MU))
     if include_kansas:
         out.append(Case("county_k2", kansas("County20"), kansas_seed("County20", 2), 2, 0, 0.10,
                         1.0))

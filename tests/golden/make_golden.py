@@ -10,6 +10,8 @@ Writes, next to this file:
 * wait_sec11.json — the reference's published per-run wait sums
   (New_plots/sec11/{alignment}B{int(100*base)}P{int(100*pop)}wait.txt, one integer each).
 * wait_ks.json — the same for plots/KS2 and plots/States/20.
+* wait_frank2.json — the same for plots/FRANK2 (Frankenstein_chain.py on the Frankengraph,
+  k=2, 100,000 yields per run, bases .3 .35 .379 and their inverses, pops .1 .5 .9).
 * flips_golden.npz — per-flip verdicts (Δcut, contiguity, population, Δboundary) on
   states drawn from oracle chains, each verdict checked here against independent
   networkx ground truth (nx.is_connected on the district subgraph, brute-force cut
@@ -71,6 +73,14 @@ def wait_fixtures():
         res[sub] = rows
     with open(os.path.join(HERE, "wait_sec11.json"), "w") as f:
         json.dump(res["New_plots/sec11"], f, indent=0)
+    frank = []
+    for f in sorted(glob.glob(os.path.join(REF, "plots/FRANK2", "*wait.txt"))):
+        m = pat.match(os.path.basename(f))
+        with open(f) as fh:
+            frank.append(dict(alignment=int(m.group(1)), base_label=int(m.group(2)),
+                              pop_label=int(m.group(3)), wait_sum=int(fh.read().strip())))
+    with open(os.path.join(HERE, "wait_frank2.json"), "w") as f:
+        json.dump(frank, f, indent=0)
     with open(os.path.join(HERE, "wait_ks.json"), "w") as f:
         json.dump({"KS2": res["plots/KS2"], "States20": res["plots/States/20"]}, f, indent=0)
 
@@ -154,6 +164,9 @@ def chain_fixtures():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["waits"]:
+        wait_fixtures()
+        sys.exit(0)
     kansas_fixtures()
     wait_fixtures()
     flip_fixtures()

@@ -102,3 +102,32 @@ def test_json_loader_casts_string_totpop():
     os.unlink(f.name)
     assert g.pop.tolist() == [5, 7] and g.n_edges == 1
     assert math.isclose(g.total_pop, 12)
+
+
+def test_frankengraph_matches_reference_construction():
+    """Frankenstein_chain.py:188-248: 50x50 grid composed with triangular_lattice_graph(50, 98)."""
+    from flipcomplexityempirical_amd.graph import (boundary_flags, frankenstein_graph,
+                                                   frankenstein_seed)
+    g = frankenstein_graph()
+    assert (g.n, g.n_edges, g.maxdeg, g.grid_w) == (5000, 12300, 6, 0)
+    idx = g.index()
+    assert idx[(0, 1)] in g.neighbors(idx[(0, 0)]) and idx[(0, -1)] in g.neighbors(idx[(0, 0)])
+    flags = boundary_flags(g)
+    rim = [k for k in g.nodes if k[0] in (0, 49) or k[1] in (50, -49)]
+    assert flags.sum() == len(rim) and all(flags[idx[k]] for k in rim)
+    sizes = [int(frankenstein_seed(g, a).sum()) for a in (0, 1, 2)]
+    assert sizes == [2450, 2500, 2450]  # diagonal, vertical, horizontal (construct_FRANK.py)
+    for a in (0, 1, 2):
+        assert O.plan_valid(g, frankenstein_seed(g, a), 2, *population_bounds(g.n, 2, 0.1))
+
+
+def test_delaunay_c4_graph_and_tree_seed():
+    """C4: ~9k-node Delaunay dual graph, lognormal populations, k=18 tree seed within 5%."""
+    from flipcomplexityempirical_amd.graph import delaunay_graph
+    g = delaunay_graph()
+    assert g.n == 9000 and 3 * g.n - 6 >= g.n_edges > 2.9 * g.n and 8 < g.maxdeg < 32
+    assert g.pop.min() >= 1 and 500 < np.median(g.pop) < 2000
+    k = 18
+    lab = recursive_tree_part(g, list(range(k)), g.total_pop / k, 0.05, seed=0)
+    lo, hi = population_bounds(g.total_pop, k, 0.05)
+    assert O.plan_valid(g, lab, k, lo, hi)  # the debt rule keeps the remainder in bounds too

@@ -49,3 +49,42 @@ def test_sec11_mean_wait_matches_reference(base, label, runs):
     ours = _ours(base, runs)
     se = np.sqrt(refv.var(ddof=1) / len(refv) + ours.var(ddof=1) / len(ours))
     assert abs(ours.mean() - refv.mean()) < 3 * se + 1e-9, (ours.mean(), refv.mean(), se)
+
+
+FRANK_BASES = {30: 0.3, 263: 1 / .379, 333: 1 / .3}  # Frankenstein_chain.py:32 bases
+
+
+def _frank_runs(base):
+    from flipcomplexityempirical_amd.graph import frankenstein_graph, frankenstein_seed
+    g = frankenstein_graph()
+    M = float(g.n ** 2 - 1)
+    out = {}
+    for a in (0, 1, 2):
+        for pop in (0.1, 0.5, 0.9):
+            lo, hi = population_bounds(g.n, 2, pop)
+            _, st, _, _ = O.run_chain(g, frankenstein_seed(g, a), 2, 0, lo, hi,
+                                      metropolis_table(base, g.maxdeg), 7,
+                                      a * 10 + int(pop * 100), 99999)
+            out[(a, int(round(pop * 100)))] = (M * st["sum_invb"][0] - st["yields"][0]) / 1e5
+    return out
+
+
+@pytest.mark.parametrize("label", sorted(FRANK_BASES))
+def test_frankengraph_mean_wait_matches_reference(label):
+    """plots/FRANK2/{a}B{b}P{p}wait.txt (Frankenstein_chain.py, the 5,000-node
+    Frankengraph, k=2, 100,000 yields): per seed alignment, the mean over the three
+    population tolerances must agree within 3 standard errors (within-alignment variance
+    pooled over both samples).  The alignments differ systematically (the horizontal seed
+    sits across the square/triangular seam), so they are compared separately."""
+    ref = json.load(open(os.path.join(GOLDEN, "wait_frank2.json")))
+    refd = {(r["alignment"], r["pop_label"]): r["wait_sum"] / 1e5 for r in ref
+            if r["base_label"] == label}
+    assert len(refd) == 9
+    ours = _frank_runs(FRANK_BASES[label])
+    groups = {a: (np.array([ours[(a, p)] for p in (10, 50, 90)]),
+                  np.array([refd[(a, p)] for p in (10, 50, 90)])) for a in (0, 1, 2)}
+    ss = sum(((o - o.mean()) ** 2).sum() + ((r - r.mean()) ** 2).sum() for o, r in groups.values())
+    s2 = ss / (len(groups) * 2 * (3 - 1))
+    se = np.sqrt(s2 * (1 / 3 + 1 / 3))
+    for a, (o, r) in groups.items():
+        assert abs(o.mean() - r.mean()) < 3 * se, (a, o, r, se)
