@@ -54,15 +54,58 @@ def totals(st):
     return {k: int(st[k].astype(np.uint64).sum()) for k in keys}
 
 
+# ------------------------------------------------------------------ workloads
+def ladder(n_bases=64, lo=0.1, hi=10.0):
+    """C5: Metropolis bases log-spaced over the reference's range (grid_chain_sec11.py:34)."""
+    return np.geomspace(lo, hi, n_bases)
+
+
+def workload(name, grid=None, k=None):
+    """(graph, seed plan, k, proposal, base, percent, default chains/GPU, description).
+
+    c3 (default, BASELINE configs[2]) 100x100 grid, k=4 quadrants, 65,536 chains/GPU
+    c2 (configs[1])   40x40 grid, k=4 quadrants, 4,096 chains
+    c4 (configs[3])   9,000-node Delaunay dual graph, lognormal pops, k=18 tree seed
+    c5 (configs[4])   200x200 grid, k=8 (2x4 blocks), 1,024 chains per base of a 64-base
+                      ladder in [0.1, 10]; 8 bases (8,192 chains) per GPU
+    frank             the 5,000-node Frankengraph of Frankenstein_chain.py, k=2, bi proposal
+    """
+    from flipcomplexityempirical_amd.graph import (block_seed, delaunay_graph, frankenstein_graph,
+                                                   frankenstein_seed, grid_graph)
+    from flipcomplexityempirical_amd.seeds import tree_seed
+    if name in ("c3", "c2"):
+        n = grid or (100 if name == "c3" else 40)
+        kk = k or 4
+        g = grid_graph(n, n)
+        init = block_seed(n, n, 2, 2) if kk == 4 else block_seed(n, n, 2, kk // 2)
+        chains = 65536 if name == "c3" else 4096
+        return (g, init, kk, "pairs", MU, 0.05, chains,
+                f"{name.upper()}: {n}x{n} grid, k={kk} block seed")
+    if name == "c4":
+        g = delaunay_graph(9000, seed=0)
+        kk = k or 18
+        return (g, tree_seed(g, kk, 0.05), kk, "pairs", MU, 0.05, 16384,
+                f"C4: 9000-node Delaunay dual graph (lognormal pops), k={kk} tree seed")
+    if name == "c5":
+        n = grid or 200
+        g = grid_graph(n, n)
+        return (g, block_seed(n, n, 2, 4), 8, "pairs", None, 0.05, 8192,
+                f"C5: {n}x{n} grid, k=8 2x4 blocks, 64-base ladder [0.1,10] x 1024 chains")
+    if name == "frank":
+        g = frankenstein_graph()
+        return (g, frankenstein_seed(g, 0), 2, "bi", 1 / .379, 0.5, 16384,
+                "Frankengraph (Frankenstein_chain.py), k=2 diagonal seed, bi proposal")
+    raise ValueError(f"unknown workload {name}")
+
+
 # ------------------------------------------------------------------ CPU baseline
 def _proxy_worker(args):
-    n, k, percent, base, seed, cid, seconds = args
+    name, percent, base, seed, cid, seconds = args
     sys.path.insert(0, ROOT)
-    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    from flipcomplexityempirical_amd.chain import PROPOSALS
     from oracle.reference_proxy import ProxyChain
-    g = grid_graph(n, n)
-    lab = block_seed(n, n, 2, 2)
-    ch = ProxyChain(g, lab, k, 1, percent, base, seed, cid)
+    g, lab, k, proposal, _, _, _, _ = workload(name)
+    ch = ProxyChain(g, lab, k, PROPOSALS[proposal], percent, base, seed, cid)
     ch.run(1)  # builds caches
     t0 = time.perf_counter()
     steps = 0
@@ -72,29 +115,26 @@ def _proxy_worker(args):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(n, k, percent, base, seed, seconds=10.0, workers=None):
+def cpu_baseline(name, desc, percent, base, seed, seconds=10.0, workers=None):
     workers = workers or min(16, os.cpu_count() or 1)
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers) as pool:
-        res = pool.map(_proxy_worker, [(n, k, percent, base, seed, i, seconds)
+        res = pool.map(_proxy_worker, [(name, percent, base, seed, i, seconds)
                                        for i in range(workers)])
     rate = sum(s / t for s, t in res)
     return {"value": rate, "unit": "flip steps/s", "cores": workers, "kind": "port",
             "sample": f"GerryChain-equivalent Python proxy (oracle/reference_proxy.py): "
-                      f"{workers} chains x ~{seconds:.0f}s, one chain per process, same C3 "
-                      f"config ({n}x{n} grid, k={k}, pairs proposal, base {base}, "
-                      f"{percent:.0%} pop); {sum(s for s, _ in res)} steps total"}
+                      f"{workers} chains x ~{seconds:.0f}s, one chain per process, same "
+                      f"workload ({desc}, base {base:.6g}, {percent:.0%} pop); "
+                      f"{sum(s for s, _ in res)} steps total"}
 
 
-def native_cpu_rate(n, k, percent, base, seed, steps=20000):
+def native_cpu_rate(g, init, k, mode, percent, base, seed, steps=20000):
     from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
-    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
     from oracle import oracle as O
-    g = grid_graph(n, n)
     lo, hi = population_bounds(g.total_pop, k, percent)
     t0 = time.perf_counter()
-    O.run_chain(g, block_seed(n, n, 2, 2), k, 1, lo, hi, metropolis_table(base, g.maxdeg), seed,
-                0, steps)
+    O.run_chain(g, init, k, mode, lo, hi, metropolis_table(base, g.maxdeg), seed, 0, steps)
     return steps / (time.perf_counter() - t0)
 
 
@@ -105,12 +145,14 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--inner", type=int, default=1000, help="flip steps per chain per launch")
-    ap.add_argument("--chains", type=int, default=65536, help="chains per GPU (weak scaling)")
-    ap.add_argument("--grid", type=int, default=100)
-    ap.add_argument("--k", type=int, default=4)
-    ap.add_argument("--base", type=float, default=MU)
-    ap.add_argument("--percent", type=float, default=0.05)
-    ap.add_argument("--proposal", default="pairs")
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5", "frank"],
+                    help="workload (see workload()); the driver's line is the default c3")
+    ap.add_argument("--chains", type=int, default=None, help="chains per GPU (weak scaling)")
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--base", type=float, default=None)
+    ap.add_argument("--percent", type=float, default=None)
+    ap.add_argument("--proposal", default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -128,17 +170,27 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
-    from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bounds
-    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    from flipcomplexityempirical_amd.chain import (PROPOSALS, Chains, DeviceGraph,
+                                                   population_bounds)
     from flipcomplexityempirical_amd.distributed import merge_histograms
 
-    n, k = args.grid, args.k
-    g = grid_graph(n, n)
-    init = block_seed(n, n, 2, 2) if k == 4 else block_seed(n, n, 2, k // 2)
-    bounds = population_bounds(g.total_pop, k, args.percent)
+    g, init, k, proposal, base, percent, chains, desc = workload(args.config, args.grid, args.k)
+    proposal = args.proposal or proposal
+    percent = args.percent if args.percent is not None else percent
+    chains = args.chains or chains
+    cid0 = rank * chains
+    if args.config == "c5" and args.base is None:
+        # whole 1,024-chain base groups per GPU: global chain id g runs ladder[g // 1024]
+        lad = ladder()
+        base = lad[(np.arange(cid0, cid0 + chains) // 1024) % len(lad)]
+        base_desc = f"ladder bases {lad[(cid0 // 1024) % 64]:.4g}..{base[-1]:.4g}"
+    else:
+        base = args.base if args.base is not None else base
+        base_desc = f"base {base:.9g}"
+    bounds = population_bounds(g.total_pop, k, percent)
     dg = DeviceGraph(g, device=local_rank)
-    ch = Chains(dg, args.chains, k, init, proposal=args.proposal, pop_bounds=bounds, base=args.base,
-                seed=args.seed, chain_id0=rank * args.chains)
+    ch = Chains(dg, chains, k, init, proposal=proposal, pop_bounds=bounds, base=base,
+                seed=args.seed, chain_id0=cid0)
 
     def barrier():
         torch.cuda.synchronize(local_rank)
@@ -175,7 +227,8 @@ def main():
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    default_c3 = (n, k, args.chains, args.inner, args.proposal) == (100, 4, 65536, 1000, "pairs")
+    default_c3 = (args.config, g.n, k, chains, args.inner, proposal) == (
+        "c3", 10000, 4, 65536, 1000, "pairs")
     if default_c3 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -195,10 +248,9 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": f"C3: {n}x{n} grid, k={k} quadrant seed, {args.chains} chains/GPU, "
-                            f"{args.proposal} proposal, base {args.base}, "
-                            f"{args.percent:.0%} pop bound, contiguity",
-                "chains_per_gpu": args.chains,
+                "workload": f"{desc}, {chains} chains/GPU, {proposal} proposal, {base_desc}, "
+                            f"{percent:.0%} pop bound, contiguity",
+                "chains_per_gpu": chains,
                 "flip_steps_per_chain_per_step": args.inner,
                 "parallelism": f"chains sharded over {world} GPU(s), RCCL histogram merge",
             },
@@ -223,9 +275,11 @@ def main():
             "hist_yields": int(hist_cut.sum()),
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(n, k, args.percent, args.base, args.seed,
+            b0 = float(np.ravel(base)[0])
+            out["cpu_baseline"] = cpu_baseline(args.config, desc, percent, b0, args.seed,
                                                seconds=args.cpu_seconds)
-            out["cpu_native_1core"] = native_cpu_rate(n, k, args.percent, args.base, args.seed)
+            out["cpu_native_1core"] = native_cpu_rate(g, init, k, PROPOSALS[proposal], percent,
+                                                      b0, args.seed)
         print(json.dumps(out), flush=True)
     ch.close()
     dg.close()

@@ -96,3 +96,18 @@ def recursive_tree_part(graph: Graph, parts: Sequence, pop_target: float, epsilo
         debt += float(pop[subset].sum()) - pop_target
         remaining = np.setdiff1d(remaining, subset)
     return lab
+
+
+def tree_seed(graph: Graph, k: int, percent: float = 0.05, seed: int = 0,
+              tries: int = 50) -> np.ndarray:
+    """A recursive_tree_part plan (labels 0..k-1) that is valid for the chain's
+    within_percent_of_ideal_population(percent) bounds; tries successive seeds."""
+    from .chain import population_bounds
+    lo, hi = population_bounds(graph.total_pop, k, percent)
+    pop = graph.pop_array()
+    for s in range(seed, seed + tries):
+        lab = recursive_tree_part(graph, list(range(k)), graph.total_pop / k, percent, seed=s)
+        p = np.bincount(lab, weights=pop, minlength=k)
+        if p.min() >= lo and p.max() <= hi:
+            return lab  # tree cuts leave every district connected
+    raise RuntimeError(f"no plan within {percent:.0%} after {tries} tree draws")

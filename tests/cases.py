@@ -18,7 +18,7 @@ from flipcomplexityempirical_amd.chain import metropolis_table, population_bound
 from flipcomplexityempirical_amd.graph import (Graph, band_seed, block_seed, delaunay_graph,
                                                frankenstein_graph, frankenstein_seed, grid_graph,
                                                sec11_graph, sec11_seed, stripe_seed)
-from flipcomplexityempirical_amd.seeds import recursive_tree_part
+from flipcomplexityempirical_amd.seeds import tree_seed
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 MU = 2.63815853
@@ -56,14 +56,7 @@ class Case:
 
 
 def c4_seed(g: Graph, k: int, percent: float = 0.05) -> np.ndarray:
-    """recursive_tree_part seed (All_States_Chain.py:232) valid for the chain's bounds."""
-    from oracle import oracle as O
-    lo, hi = population_bounds(g.total_pop, k, percent)
-    for s in range(50):
-        lab = recursive_tree_part(g, list(range(k)), g.total_pop / k, percent, seed=s)
-        if O.plan_valid(g, lab, k, lo, hi):
-            return lab
-    raise RuntimeError("no valid tree seed")
+    return tree_seed(g, k, percent)
 
 
 def cases(include_kansas: bool = True):
