@@ -165,6 +165,36 @@ class Chains:
     def pops(self) -> np.ndarray:
         return self._read(_lib.READ_POPS, np.empty((self.n_chains, self.k), np.int64))
 
+    # ------------------------------------------------------------- spatial maps
+    def enable_maps(self, label_values: Optional[Sequence[int]] = None) -> None:
+        """Track the reference driver's per-edge / per-node maps on every chain
+        (grid_chain_sec11.py:383-384, 396-400).  ``label_values``: the GerryChain
+        assignment value of each district index (default 0..k-1; {-1, 1} for the
+        reference's k=2 plans).  Call before the first run."""
+        lv = None
+        if label_values is not None:
+            lv = np.ascontiguousarray(label_values, np.int64)
+            if len(lv) != self.k:
+                raise ValueError(f"need {self.k} label values")
+        check(_lib.load().fw_chains_enable_maps(self._h, ptr(lv)))
+        self.label_values = (np.arange(self.k, dtype=np.int64) if lv is None else lv)
+
+    MAPS = {"cut_times": _lib.MAP_CUT_TIMES, "num_flips": _lib.MAP_NUM_FLIPS,
+            "part_sum": _lib.MAP_PART_SUM, "last_flipped": _lib.MAP_LAST_FLIPPED}
+
+    def read_map(self, what: str, chains=None, total: bool = False,
+                 finalize: bool = False) -> np.ndarray:
+        """int64 map ``what`` (cut_times [E], num_flips / part_sum / last_flipped [n]) of
+        chains ``range(*chains)`` (default all) as [n_chains, len], or summed over them
+        (``total``).  ``finalize`` applies grid_chain_sec11.py:416-419 to part_sum."""
+        lo, hi = (0, self.n_chains) if chains is None else (int(chains[0]), int(chains[1]))
+        m = self.dgraph.n_edges if what == "cut_times" else self.dgraph.n
+        out = np.empty(m if total else (hi - lo, m), np.int64)
+        flags = (_lib.MAP_SUM if total else 0) | (_lib.MAP_FINALIZE if finalize else 0)
+        check(_lib.load().fw_chains_read_map(self._h, self.MAPS[what], lo, hi - lo, flags,
+                                             ptr(out), out.nbytes))
+        return out
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.load().fw_chains_destroy(self._h)

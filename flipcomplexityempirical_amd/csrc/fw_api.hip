@@ -81,11 +81,15 @@ struct fw_graph {
   int32_t* d_rowptr = nullptr;
   int32_t* d_col = nullptr;
   int64_t* d_pop = nullptr;
+  int32_t* d_eid = nullptr;  // [nnz] canonical edge id per CSR entry
+  int32_t* d_eu = nullptr;   // [E] canonical edge endpoints (u < w)
+  int32_t* d_ew = nullptr;
   int64_t popof(int x) const { return pop.empty() ? 1 : pop[x]; }
   FwGraphDev dev() const {
     FwGraphDev g;
     g.rowptr = d_rowptr;
     g.col = d_col;
+    g.eid = d_eid;
     g.pop = d_pop;
     g.n = n;
     g.nedges = nnz / 2;
@@ -113,6 +117,15 @@ struct fw_chains {
   unsigned long long* d_hist_b = nullptr;
   uint32_t* d_spill = nullptr;
   int32_t* d_next = nullptr;
+  uint64_t max_yields = 0;  // upper bound on any chain's yield count (maps need < 2^32)
+  bool ran = false;
+  // spatial observables (fw_chains_enable_maps)
+  int64_t* d_acc = nullptr;
+  uint32_t* d_nf = nullptr;
+  uint32_t* d_lf = nullptr;
+  int64_t* d_ps = nullptr;
+  int32_t* d_pend = nullptr;
+  int64_t* d_labval = nullptr;
 };
 
 namespace {
@@ -194,7 +207,7 @@ extern "C" {
 
 const char* fw_last_error(void) { return g_err.c_str(); }
 
-int32_t fw_version(void) { return 0x000100; }
+int32_t fw_version(void) { return 0x000200; }
 
 int32_t fw_device_count(void) {
   int c = 0;
@@ -245,9 +258,27 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
     delete g;
     return fail(FW_EHIP, "hipSetDevice(%d) failed", device);
   }
+  // canonical edge ids: undirected pairs (u < w) numbered in CSR row order
+  std::vector<int32_t> eid(std::max(nnz, 1)), eu, ew;
+  for (int x = 0; x < n; ++x)
+    for (int t = rowptr[x]; t < rowptr[x + 1]; ++t) {
+      const int y = col[t];
+      if (y > x) {
+        eid[t] = (int32_t)eu.size();
+        eu.push_back(x);
+        ew.push_back(y);
+      } else {  // (y, x) was numbered in row y
+        const int32_t* q = std::lower_bound(col + rowptr[y], col + rowptr[y + 1], x);
+        eid[t] = eid[q - col];
+      }
+    }
+  const size_t ne = std::max<size_t>(eu.size(), 1);
   hipError_t e1 = hipMalloc(&g->d_rowptr, sizeof(int32_t) * (n + 1));
   hipError_t e2 = hipMalloc(&g->d_col, sizeof(int32_t) * std::max(nnz, 1));
   hipError_t e3 = g->pop.empty() ? hipSuccess : hipMalloc(&g->d_pop, sizeof(int64_t) * n);
+  if (e3 == hipSuccess) e3 = hipMalloc(&g->d_eid, sizeof(int32_t) * eid.size());
+  if (e3 == hipSuccess) e3 = hipMalloc(&g->d_eu, sizeof(int32_t) * ne);
+  if (e3 == hipSuccess) e3 = hipMalloc(&g->d_ew, sizeof(int32_t) * ne);
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
     fw_graph_destroy(g);
     return fail(FW_EHIP, "hipMalloc failed for graph");
@@ -258,6 +289,14 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   if (g->d_pop)
     up &= hipMemcpy(g->d_pop, g->pop.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice) ==
           hipSuccess;
+  up &= hipMemcpy(g->d_eid, eid.data(), sizeof(int32_t) * eid.size(), hipMemcpyHostToDevice) ==
+        hipSuccess;
+  if (!eu.empty()) {
+    up &= hipMemcpy(g->d_eu, eu.data(), sizeof(int32_t) * eu.size(), hipMemcpyHostToDevice) ==
+          hipSuccess;
+    up &= hipMemcpy(g->d_ew, ew.data(), sizeof(int32_t) * ew.size(), hipMemcpyHostToDevice) ==
+          hipSuccess;
+  }
   if (!up || hipDeviceSynchronize() != hipSuccess) {
     fw_graph_destroy(g);
     return fail(FW_EHIP, "graph upload failed");
@@ -272,6 +311,9 @@ void fw_graph_destroy(fw_graph* g) {
   if (g->d_rowptr) (void)hipFree(g->d_rowptr);
   if (g->d_col) (void)hipFree(g->d_col);
   if (g->d_pop) (void)hipFree(g->d_pop);
+  if (g->d_eid) (void)hipFree(g->d_eid);
+  if (g->d_eu) (void)hipFree(g->d_eu);
+  if (g->d_ew) (void)hipFree(g->d_ew);
   delete g;
 }
 
@@ -289,8 +331,9 @@ void fw_chains_destroy(fw_chains* c) {
   if (!c) return;
   (void)hipSetDevice(c->g->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_hist_cut, c->d_hist_b,
-                  c->d_spill, c->d_next};
+  void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr,  c->d_hist_cut, c->d_hist_b,
+                  c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
+                  c->d_pend,   c->d_labval};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -444,6 +487,10 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
   if (!c || steps < 0 || max_retries <= 0) return fail(FW_EINVAL, "fw_chains_run: bad arguments");
   HIPCHK(hipSetDevice(c->g->device));
   if (steps == 0) return FW_OK;
+  if (c->d_acc && c->max_yields + (uint64_t)steps + 1 >= 0xFFFFFFFFull)
+    return fail(FW_EUNSUPPORTED, "spatial maps hold yield indices below 2^32");
+  c->max_yields += (uint64_t)steps + (c->ran ? 0 : 1);
+  c->ran = true;
   c->p.steps = steps;
   c->p.max_retries = max_retries;
   HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
@@ -557,7 +604,108 @@ int fw_chains_reset_observables(fw_chains* c) {
   HIPCHK(hipMemset(c->d_hist_cut, 0,
                    sizeof(unsigned long long) * (c->g->nnz / 2 + 1 + FW_HIST_PAD)));
   HIPCHK(hipMemset(c->d_hist_b, 0, sizeof(unsigned long long) * (c->g->n + 1 + FW_HIST_PAD)));
+  if (c->d_acc) {  // maps restart from the current plans (yield indices restart at 0)
+    const size_t C = (size_t)c->n_chains, n = (size_t)c->g->n, E = (size_t)c->g->nnz / 2;
+    HIPCHK(hipMemset(c->d_acc, 0, sizeof(int64_t) * std::max<size_t>(C * E, 1)));
+    HIPCHK(hipMemset(c->d_nf, 0, sizeof(uint32_t) * C * n));
+    HIPCHK(hipMemset(c->d_lf, 0, sizeof(uint32_t) * C * n));
+    if (fw_launch_map_init(c->p, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(FW_EHIP, "map re-init failed");
+    c->max_yields = 0;
+  }
   return FW_OK;
+}
+
+int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values) {
+  if (!c) return fail(FW_EINVAL, "null handle");
+  if (c->ran) return fail(FW_ESTATE, "enable the spatial maps before the first run");
+  if (c->d_acc) return FW_OK;
+  HIPCHK(hipSetDevice(c->g->device));
+  const size_t C = (size_t)c->n_chains, n = (size_t)c->g->n, E = (size_t)c->g->nnz / 2;
+  std::vector<int64_t> lv(c->k);
+  for (int d = 0; d < c->k; ++d) lv[d] = label_values ? label_values[d] : d;
+  bool ok = hipMalloc(&c->d_acc, sizeof(int64_t) * std::max<size_t>(C * E, 1)) == hipSuccess &&
+            hipMalloc(&c->d_nf, sizeof(uint32_t) * C * n) == hipSuccess &&
+            hipMalloc(&c->d_lf, sizeof(uint32_t) * C * n) == hipSuccess &&
+            hipMalloc(&c->d_ps, sizeof(int64_t) * C * n) == hipSuccess &&
+            hipMalloc(&c->d_pend, sizeof(int32_t) * 4 * C) == hipSuccess &&
+            hipMalloc(&c->d_labval, sizeof(int64_t) * lv.size()) == hipSuccess;
+  if (!ok) {
+    void* bufs[] = {c->d_acc, c->d_nf, c->d_lf, c->d_ps, c->d_pend, c->d_labval};
+    for (void* b : bufs)
+      if (b) (void)hipFree(b);
+    c->d_acc = nullptr;
+    c->d_nf = c->d_lf = nullptr;
+    c->d_ps = nullptr;
+    c->d_pend = nullptr;
+    c->d_labval = nullptr;
+    return fail(FW_ENOMEM, "spatial maps need %zu MB of device memory",
+                (C * (8 * E + 16 * n)) >> 20);
+  }
+  HIPCHK(hipMemcpy(c->d_labval, lv.data(), sizeof(int64_t) * lv.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemsetAsync(c->d_acc, 0, sizeof(int64_t) * std::max<size_t>(C * E, 1), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_nf, 0, sizeof(uint32_t) * C * n, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_lf, 0, sizeof(uint32_t) * C * n, c->stream));
+  FwRunParams& p = c->p;
+  p.m_acc = c->d_acc;
+  p.m_nf = c->d_nf;
+  p.m_lf = c->d_lf;
+  p.m_ps = c->d_ps;
+  p.m_pend = c->d_pend;
+  p.m_labval = c->d_labval;
+  if (fw_launch_map_init(p, c->stream) != 0)
+    return fail(FW_EHIP, "map init launch failed: %s", hipGetErrorString(hipGetLastError()));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return FW_OK;
+}
+
+int fw_chains_read_map(fw_chains* c, int32_t what, int32_t chain0, int32_t n_chains, int32_t flags,
+                       int64_t* dst, size_t bytes) {
+  if (!c || !dst) return fail(FW_EINVAL, "fw_chains_read_map: null");
+  if (!c->d_acc) return fail(FW_ESTATE, "spatial maps are not enabled");
+  if (what < FW_MAP_CUT_TIMES || what > FW_MAP_LAST_FLIPPED)
+    return fail(FW_EINVAL, "unknown map %d", what);
+  if (chain0 < 0 || n_chains <= 0 || (int64_t)chain0 + n_chains > c->n_chains)
+    return fail(FW_EINVAL, "chain range [%d, %d) outside [0, %d)", chain0, chain0 + n_chains,
+                c->n_chains);
+  const int E = c->g->nnz / 2, n = c->g->n;
+  const size_t M = what == FW_MAP_CUT_TIMES ? (size_t)E : (size_t)n;
+  const bool sum = (flags & FW_MAP_SUM) != 0;
+  const size_t need = sizeof(int64_t) * M * (sum ? 1 : (size_t)n_chains);
+  if (bytes < need) return fail(FW_EINVAL, "map needs %zu bytes", need);
+  if (M == 0) return FW_OK;
+  HIPCHK(hipSetDevice(c->g->device));
+  int64_t* d_out = nullptr;
+  HIPCHK(hipMalloc(&d_out, need));
+  FwMapRead m{};
+  m.acc = c->d_acc;
+  m.nf = c->d_nf;
+  m.lf = c->d_lf;
+  m.ps = c->d_ps;
+  m.pend = c->d_pend;
+  m.labval = c->d_labval;
+  m.labels = c->d_labels;
+  m.lab_stride = c->p.lab_stride;
+  m.stats = c->d_stats;
+  m.eu = c->g->d_eu;
+  m.ew = c->g->d_ew;
+  m.n = n;
+  m.E = E;
+  m.lb = c->lb;
+  m.what = what;
+  m.sum = sum ? 1 : 0;
+  m.finalize = (flags & FW_MAP_FINALIZE) ? 1 : 0;
+  m.chain0 = chain0;
+  m.n_chains = n_chains;
+  m.out = d_out;
+  int rc = FW_OK;
+  if (fw_launch_map_read(m, c->stream) != 0)
+    rc = fail(FW_EHIP, "map read launch failed: %s", hipGetErrorString(hipGetLastError()));
+  else if (hipMemcpyAsync(dst, d_out, need, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+           hipStreamSynchronize(c->stream) != hipSuccess)
+    rc = fail(FW_EHIP, "map download failed");
+  (void)hipFree(d_out);
+  return rc;
 }
 
 int fw_eval_flips(fw_graph* g, const int16_t* labels, int32_t k, const int32_t* v,

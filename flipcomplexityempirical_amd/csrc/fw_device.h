@@ -188,6 +188,52 @@ __device__ __forceinline__ int window_verdict(uint64_t A) {
 // window cell c in [0,48) (v skipped) -> bit position and (di, dj) offsets from v
 __device__ __forceinline__ int window_pos(int c) { return c < 24 ? c : c + 1; }
 
+// ---------------------------------------------------------------- spatial observables
+// Canonical id of a grid edge (node (r,c) to its right / lower neighbour): the position
+// of the pair in CSR row order of the row-major W x H grid (include/flipwalk.h).
+__device__ __forceinline__ int grid_eid_right(int r, int c, int W, int H) {
+  return r * (2 * W - 1) + c * (1 + (r < H - 1 ? 1 : 0));
+}
+__device__ __forceinline__ int grid_eid_down(int r, int c, int W, int H) {
+  return grid_eid_right(r, c, W, H) + (c < W - 1 ? 1 : 0);
+}
+
+// The pending run of the current state's creating flip (f < 0: the initial state).
+struct Pend {
+  int32_t f, lab;
+  uint32_t t0;  // yield index at which the state was first yielded
+};
+
+__device__ __forceinline__ Pend pend_load(const FwRunParams& p, int c) {
+  if (p.m_acc == nullptr) return Pend{-1, 0, 0u};
+  const int32_t* pe = p.m_pend + 4 * (size_t)c;
+  return Pend{pe[0], pe[1], (uint32_t)pe[2]};
+}
+__device__ __forceinline__ void pend_store(const FwRunParams& p, int c, const Pend& pd) {
+  int32_t* pe = p.m_pend + 4 * (size_t)c;
+  pe[0] = pd.f;
+  pe[1] = pd.lab;
+  pe[2] = (int32_t)pd.t0;
+}
+// Edge e of chain c changes status at yield t (the new state's index):
+// cut_times = acc + [cut now] * yields, so becoming cut subtracts t, uncut adds t.
+__device__ __forceinline__ void map_edge(const FwRunParams& p, int c, int e, bool becomes_cut,
+                                         int64_t t) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p.m_acc + (size_t)c * p.g.nedges + e),
+            (unsigned long long)(becomes_cut ? -t : t));
+}
+// The run of pd.f (yields pd.t0 .. t-1) ends: the reference's per-yield updates
+// part_sum[f] -= L*(t_i - last_flipped); last_flipped = t_i; num_flips += 1, summed.
+__device__ __forceinline__ void map_run_end(const FwRunParams& p, int c, const Pend& pd,
+                                            int64_t t) {
+  if (pd.f < 0) return;
+  const size_t o = (size_t)c * p.g.n + pd.f;
+  atomicAdd(p.m_nf + o, (uint32_t)(t - (int64_t)pd.t0));
+  const uint32_t old = atomicExch(p.m_lf + o, (uint32_t)(t - 1));
+  atomicAdd(reinterpret_cast<unsigned long long*>(p.m_ps + o),
+            (unsigned long long)(-p.m_labval[pd.lab] * ((t - 1) - (int64_t)old)));
+}
+
 // ---------------------------------------------------------------- chain context
 // Grid lane roles for v's neighbourhood: 0 v, 1 up, 2 left, 3 right, 4 down
 // (= CSR order of v's neighbours), 5 NE, 6 SE, 7 SW, 8 NW.

@@ -399,6 +399,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0, n_sdeg = 0, n_adeg = 0, n_bchg = 0;
     uint32_t n_yield = 0, retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
+    Pend pend = pend_load(p, cc);
     lds_order();
 
     // ---- derive group sums, cut / boundary / proposal-set counts (per row)
@@ -709,6 +710,18 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (valid && p.trace && q == 0)
         p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
       n_steps += valid ? 1u : 0u;
+      if (p.m_acc != nullptr && accepted) {  // spatial observables: fire-and-forget atomics
+        const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
+        if (q >= 1 && q <= 4 && h.x >= 0 && (h.lx == a || h.lx == d)) {
+          const int e = q == 1   ? grid_eid_down(vr - 1, vc, W, H)
+                        : q == 2 ? grid_eid_right(vr, vc - 1, W, H)
+                        : q == 3 ? grid_eid_right(vr, vc, W, H)
+                                 : grid_eid_down(vr, vc, W, H);
+          map_edge(p, c, e, h.lx == a, t);
+        }
+        if (q == 0) map_run_end(p, c, pend, t);
+        pend = Pend{v, (int32_t)d, (uint32_t)t};
+      }
 
       // ---- commit (accepting rows)
       uint32_t wo = 0, wn = 0;
@@ -769,6 +782,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
       if (q < k) p.pops[(size_t)c * k + q] = pops;
+      if (q == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
       if (q == 0) {
         stp->attempts = attempts;
         stp->steps += n_steps;

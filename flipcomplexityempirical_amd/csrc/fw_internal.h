@@ -15,6 +15,7 @@
 struct FwGraphDev {
   const int32_t* rowptr;  // [n+1]
   const int32_t* col;     // [nnz]
+  const int32_t* eid;     // [nnz] canonical edge id of each CSR entry
   const int64_t* pop;     // [n] or nullptr (unit populations)
   int32_t n, nedges, maxdeg;
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)
@@ -52,6 +53,34 @@ struct FwRunParams {
   int32_t off_scr, scr_bytes;  // 4-bit search scratch
   int32_t off_list16, qcap16;  // shared visit list
   int32_t lds16;               // dynamic LDS bytes per workgroup
+  // spatial observables (nullptr: off).  Per chain c: acc [E] (int64: sum of -t when an
+  // edge becomes cut and +t when it becomes uncut, so cut_times = acc + [cut now] * Y),
+  // nf / lf [n] (num_flips, last_flipped of finished runs), ps [n] (part_sum), and the
+  // pending run {node, district, first yield, -} of the current state's creating flip.
+  int64_t* m_acc;
+  uint32_t* m_nf;
+  uint32_t* m_lf;
+  int64_t* m_ps;
+  int32_t* m_pend;
+  const int64_t* m_labval;     // [k] GerryChain label values
+};
+
+// fw_chains_read_map: finalise maps of a chain range (see include/flipwalk.h)
+struct FwMapRead {
+  const int64_t* acc;
+  const uint32_t* nf;
+  const uint32_t* lf;
+  const int64_t* ps;
+  const int32_t* pend;
+  const int64_t* labval;
+  const uint8_t* labels;
+  int64_t lab_stride;
+  const fw_chain_stats* stats;
+  const int32_t* eu;  // [E] edge endpoints, canonical order
+  const int32_t* ew;
+  int32_t n, E, lb, what, sum, finalize;
+  int32_t chain0, n_chains;
+  int64_t* out;
 };
 
 struct FwEvalParams {
@@ -73,6 +102,8 @@ struct FwEvalParams {
 };
 
 // Host-side launchers implemented in fw_kernels.hip.
+int fw_launch_map_init(const FwRunParams& p, void* stream);
+int fw_launch_map_read(const FwMapRead& m, void* stream);
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);

@@ -76,6 +76,7 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0;
     uint32_t n_sdeg = 0, n_adeg = 0, n_bchg = 0, n_yield = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
+    Pend pend = pend_load(p, c);
     __syncthreads();
 
     // ---- derive group sums, cut count, boundary count, proposal-set size
@@ -201,6 +202,27 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       // ---- Metropolis (cut_accept, grid_chain_sec11.py:171-179)
       const bool accepted = u53(x.x2, x.x3) < rdl_f64(thr_l, dcut + D);
       if (p.trace && lane == 0) p.trace[(size_t)c * p.steps + s] = accepted ? v * 64 + (int)d : -1;
+      if (accepted && p.m_acc != nullptr) {  // spatial observables: fire-and-forget atomics
+        const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
+        const bool nbl = GRID ? (lane >= 1 && lane <= 4 && h.x >= 0) : (lane >= 1 && lane <= dv);
+        if (nbl && (h.lx == a || h.lx == d)) {
+          int e;
+          if constexpr (GRID) {
+            int vr, vc;
+            C.divmod(v, vr, vc);
+            const int W = p.g.gw, H = p.g.gh;
+            e = lane == 1   ? grid_eid_down(vr - 1, vc, W, H)
+                : lane == 2 ? grid_eid_right(vr, vc - 1, W, H)
+                : lane == 3 ? grid_eid_right(vr, vc, W, H)
+                            : grid_eid_down(vr, vc, W, H);
+          } else {
+            e = p.g.eid[p.g.rowptr[v] + lane - 1];
+          }
+          map_edge(p, c, e, h.lx == a, t);
+        }
+        if (lane == 0) map_run_end(p, c, pend, t);
+        pend = Pend{v, (int32_t)d, (uint32_t)t};
+      }
       if (accepted) {
         n_acc += 1;
         n_adeg += (uint32_t)dv;
@@ -232,6 +254,7 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       for (int i = lane; i < p.lab_bytes / 16; i += WAVE) dst[i] = src[i];
       if (lane < k) p.pops[(size_t)c * k + lane] = pops;
     }
+    if (lane == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
     if (lane == 0) {
       stp->attempts = attempts;
       stp->steps += n_steps;
@@ -307,6 +330,69 @@ __global__ __launch_bounds__(64) void fw_eval_kernel(FwEvalParams p) {
   }
 }
 
+// ---------------------------------------------------------------- spatial-observable maps
+__device__ __forceinline__ uint32_t glabel(const uint8_t* lab, int lb, int x) {
+  const int bit = x * lb;
+  return (uint32_t)(lab[bit >> 3] >> (bit & 7)) & ((1u << lb) - 1u);
+}
+
+// part_sum := label value of the initial plan (grid_chain_sec11.py:219); pending runs none
+__global__ void fw_map_init_kernel(FwRunParams p, int lb) {
+  const size_t total = (size_t)p.n_chains * (size_t)p.g.n;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t c = i / (size_t)p.g.n;
+    const int x = (int)(i - c * (size_t)p.g.n);
+    p.m_ps[i] = p.m_labval[glabel(p.labels + c * p.lab_stride, lb, x)];
+    if (x == 0) {
+      p.m_pend[4 * c] = -1;
+      p.m_pend[4 * c + 1] = 0;
+      p.m_pend[4 * c + 2] = 0;
+      p.m_pend[4 * c + 3] = 0;
+    }
+  }
+}
+
+// Maps current through each chain's last yield Y: open cut intervals and the pending run
+// of the current state's creating flip are closed at Y - 1 (without changing the state).
+__global__ void fw_map_read_kernel(FwMapRead m) {
+  const int M = m.what == FW_MAP_CUT_TIMES ? m.E : m.n;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+    int64_t total = 0;
+    for (int cc = 0; cc < m.n_chains; ++cc) {
+      const size_t c = (size_t)(m.chain0 + cc);
+      const int64_t Y = (int64_t)m.stats[c].yields;
+      const uint8_t* lab = m.labels + c * m.lab_stride;
+      int64_t val;
+      if (m.what == FW_MAP_CUT_TIMES) {
+        const bool cut = glabel(lab, m.lb, m.eu[i]) != glabel(lab, m.lb, m.ew[i]);
+        val = m.acc[c * m.E + i] + (cut ? Y : 0);
+      } else {
+        const int32_t* pe = m.pend + 4 * c;
+        int64_t nf = m.nf[c * m.n + i], lf = m.lf[c * m.n + i], ps = m.ps[c * m.n + i];
+        if (pe[0] == i && Y > (int64_t)(uint32_t)pe[2]) {  // pending run [t0, Y-1]
+          nf += Y - (int64_t)(uint32_t)pe[2];
+          ps -= m.labval[pe[1]] * ((Y - 1) - lf);
+          lf = Y - 1;
+        }
+        if (m.what == FW_MAP_NUM_FLIPS) {
+          val = nf;
+        } else if (m.what == FW_MAP_LAST_FLIPPED) {
+          val = lf;
+        } else {
+          val = ps;  // grid_chain_sec11.py:416-419
+          if (m.finalize && lf == 0) val = Y * m.labval[glabel(lab, m.lb, i)];
+        }
+      }
+      if (m.sum)
+        total += val;
+      else
+        m.out[(size_t)cc * M + i] = val;
+    }
+    if (m.sum) m.out[i] = total;
+  }
+}
+
 template <int LB, bool GRID, int MODE>
 void* pick_per(int G) {
   if (G <= 64 * 2) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2>);
@@ -350,6 +436,18 @@ int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   void* args[] = {const_cast<FwRunParams*>(&p)};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes, (hipStream_t)stream);
   return e == hipSuccess ? 0 : -1;
+}
+
+int fw_launch_map_init(const FwRunParams& p, void* stream) {
+  hipLaunchKernelGGL(fw_map_init_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, p, p.lb);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int fw_launch_map_read(const FwMapRead& m, void* stream) {
+  const int M = m.what == FW_MAP_CUT_TIMES ? m.E : m.n;
+  const int blocks = (M + 255) / 256;
+  hipLaunchKernelGGL(fw_map_read_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, m);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream) {

@@ -73,6 +73,19 @@ extern "C" {
 #define FW_READ_HIST_B 3   /* uint64 [n+1]        yields with |B| = i         */
 #define FW_READ_POPS 4     /* int64  [n_chains][k] district populations       */
 
+/* ---- spatial observables (fw_chains_enable_maps / fw_chains_read_map) ------
+ * The reference driver's per-edge and per-node maps, updated once per yield
+ * (grid_chain_sec11.py:383-384 cut_times, :396-400 part_sum / last_flipped /
+ * num_flips, finalised at :416-419; the same code in Frankenstein_chain.py and
+ * All_States_Chain.py).  Edges are indexed canonically: undirected (u < w) pairs
+ * in CSR row order.  Values are int64.                                           */
+#define FW_MAP_CUT_TIMES 0    /* [n_edges] yields in which the edge was cut          */
+#define FW_MAP_NUM_FLIPS 1    /* [n] yields whose state was created by flipping node */
+#define FW_MAP_PART_SUM 2     /* [n] part_sum (starts at the initial label value)    */
+#define FW_MAP_LAST_FLIPPED 3 /* [n] last such yield index (0: never)                */
+#define FW_MAP_SUM 1          /* flag: sum over the chain range into one row          */
+#define FW_MAP_FINALIZE 2     /* flag: PART_SUM of never-flipped nodes := yields*label */
+
 /* Per-chain counters and running observables (the per-yield block of
  * grid_chain_sec11.py:366-402, reduced to sums; one struct per chain). */
 typedef struct fw_chain_stats {
@@ -104,7 +117,7 @@ typedef struct fw_chains fw_chains;
 /* Thread-local description of the last error on this thread. */
 const char* fw_last_error(void);
 
-/* Library/ABI version, e.g. 0x000100 for 0.1.0. */
+/* Library/ABI version, e.g. 0x000200 for 0.2.0 (0.2: spatial maps). */
 int32_t fw_version(void);
 
 /* Number of visible HIP devices (0 when none; never fails). */
@@ -164,6 +177,19 @@ int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes);
 
 /* Zero the per-chain sums and the yield histograms (not the chain states). */
 int fw_chains_reset_observables(fw_chains* c);
+
+/* Turn on the spatial observables for every chain (before the first run).
+ * label_values [k] are the GerryChain assignment values of districts 0..k-1
+ * (e.g. {-1, 1} for the reference's k=2 plans); NULL means 0..k-1.  Costs
+ * 8*n_edges + 16*n bytes of HBM per chain.  Yields per chain must stay below 2^32. */
+int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values);
+
+/* Read a map (FW_MAP_*) of chains [chain0, chain0 + n_chains) as int64
+ * [n_chains][len], or with FW_MAP_SUM its sum over those chains [len]; len is
+ * n_edges for FW_MAP_CUT_TIMES and n otherwise.  Values are current through the
+ * last yield; FW_MAP_FINALIZE applies the reference's end-of-run rule. */
+int fw_chains_read_map(fw_chains* c, int32_t what, int32_t chain0, int32_t n_chains,
+                       int32_t flags, int64_t* dst, size_t bytes);
 
 /* Batched per-flip evaluation on ONE state — the bit-exact per-step contract
  * (cut_edges updater, single_flip_contiguous, Bounds, b_nodes_bi):

@@ -110,7 +110,28 @@ typedef struct {
   fw_chain_stats st;
   uint64_t* hist_cut; /* may be NULL */
   uint64_t* hist_b;   /* may be NULL */
+  struct orc_maps* maps; /* may be NULL */
 } chain_t;
+
+/* The reference driver's spatial observables, updated once per yield exactly as
+ * grid_chain_sec11.py:383-384 and :396-400 do (Frankenstein_chain.py:413-425 and
+ * All_States_Chain.py:334-342 are the same code):
+ *   for edge in part["cut_edges"]: cut_times[edge] += 1
+ *   if part.flips is not None:     f = the node of the state's creating flip
+ *       part_sum[f] -= assignment[f] * (t - last_flipped[f]); last_flipped[f] = t;
+ *       num_flips[f] += 1
+ * where t is the yield index (0 = initial state, whose flips is None) and a state
+ * re-yielded after a Metropolis rejection keeps its creating flip.  Edges are indexed in
+ * canonical order (u < w, CSR row order); assignment values come from label_value[k]. */
+typedef struct orc_maps {
+  int64_t* cut_times;        /* [n_edges] */
+  int64_t* num_flips;        /* [n] */
+  int64_t* part_sum;         /* [n], initialised by the caller to label_value[initial] */
+  int64_t* last_flipped;     /* [n] */
+  const int64_t* label_value; /* [k] */
+  int32_t cur_f;             /* creating flip of the current state, -1: none (initial) */
+  int32_t pad;
+} orc_maps;
 
 static inline int64_t popof(const graph_t* g, int32_t v) { return g->pop ? g->pop[v] : 1; }
 
@@ -357,7 +378,28 @@ static int16_t target_of(const chain_t* c, int32_t v, int64_t j) {
   return prev;
 }
 
+static void maps_yield(chain_t* c) {
+  orc_maps* m = c->maps;
+  const graph_t* g = &c->g;
+  const int64_t t = (int64_t)c->st.yields; /* index of the state being yielded */
+  int64_t e_id = 0;
+  for (int32_t x = 0; x < g->n; ++x)
+    for (int32_t e = g->rowptr[x]; e < g->rowptr[x + 1]; ++e) {
+      const int32_t y = g->col[e];
+      if (y <= x) continue;
+      if (c->lab[x] != c->lab[y]) m->cut_times[e_id]++;
+      ++e_id;
+    }
+  if (m->cur_f >= 0) {
+    const int32_t f = m->cur_f;
+    m->part_sum[f] -= m->label_value[c->lab[f]] * (t - m->last_flipped[f]);
+    m->last_flipped[f] = t;
+    m->num_flips[f] += 1;
+  }
+}
+
 static void yield_obs(chain_t* c) {
+  if (c->maps) maps_yield(c);
   c->st.yields++;
   c->st.sum_cut += c->st.cut;
   c->st.sum_bnodes += c->st.bnodes;
@@ -442,11 +484,12 @@ static void teardown(chain_t* c) {
  * Metropolis draw rejected) — used to replay trajectories in tests.
  * Returns 0, or -1 on allocation failure.
  */
-int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop, int32_t n,
-                  int32_t grid_w, int32_t k, int32_t mode, int64_t pop_lo, int64_t pop_hi,
-                  const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
-                  fw_chain_stats* stats, int64_t steps, int32_t max_retries, uint64_t* hist_cut,
-                  uint64_t* hist_b, int32_t* trace, int64_t* pops_out) {
+int orc_run_chain_maps(const int32_t* rowptr, const int32_t* col, const int64_t* pop, int32_t n,
+                       int32_t grid_w, int32_t k, int32_t mode, int64_t pop_lo, int64_t pop_hi,
+                       const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
+                       fw_chain_stats* stats, int64_t steps, int32_t max_retries,
+                       uint64_t* hist_cut, uint64_t* hist_b, int32_t* trace, int64_t* pops_out,
+                       orc_maps* maps) {
   chain_t c;
   if (setup(&c, rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr)) {
     teardown(&c);
@@ -458,6 +501,7 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
   c.st = *stats;
   c.hist_cut = hist_cut;
   c.hist_b = hist_b;
+  c.maps = maps;
   derive(&c);
   const int32_t D = c.g.maxdeg;
   if (c.st.yields == 0 && c.st.attempts == 0) yield_obs(&c);
@@ -507,6 +551,7 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
       c.st.accepts++;
       c.st.acc_deg += (uint64_t)(rowptr[v + 1] - rowptr[v]);
       c.st.n_bchg += (uint64_t)commit(&c, v, b, dcut);
+      if (maps) maps->cur_f = v;
     }
     if (trace) trace[s] = accepted ? v : -1;
     yield_obs(&c);
@@ -516,6 +561,16 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
   *stats = c.st;
   teardown(&c);
   return 0;
+}
+
+int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop, int32_t n,
+                  int32_t grid_w, int32_t k, int32_t mode, int64_t pop_lo, int64_t pop_hi,
+                  const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
+                  fw_chain_stats* stats, int64_t steps, int32_t max_retries, uint64_t* hist_cut,
+                  uint64_t* hist_b, int32_t* trace, int64_t* pops_out) {
+  return orc_run_chain_maps(rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr, seed,
+                            chain_id, labels, stats, steps, max_retries, hist_cut, hist_b, trace,
+                            pops_out, NULL);
 }
 
 /* Per-flip evaluation on one state (the fw_eval_flips contract). */

@@ -65,6 +65,8 @@ def lib():
             ctypes.c_int64, ctypes.c_int32, _P, _P, _P, _P,
         ]
         L.orc_run_chain.restype = ctypes.c_int
+        L.orc_run_chain_maps.argtypes = L.orc_run_chain.argtypes + [_P]
+        L.orc_run_chain_maps.restype = ctypes.c_int
         L.orc_eval_flips.argtypes = [
             _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
             ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P,
@@ -96,21 +98,55 @@ def new_stats(n=1):
     return np.zeros(n, dtype=STATS_DTYPE)
 
 
+class _OrcMaps(ctypes.Structure):
+    _fields_ = [("cut_times", _P), ("num_flips", _P), ("part_sum", _P), ("last_flipped", _P),
+                ("label_value", _P), ("cur_f", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class Maps:
+    """The reference driver's per-edge / per-node observables of one chain
+    (grid_chain_sec11.py:383-384, 396-400), updated per yield by the C oracle."""
+
+    def __init__(self, graph, init_labels, label_values):
+        self.label_value = np.ascontiguousarray(label_values, np.int64)
+        self.cut_times = np.zeros(graph.n_edges, np.int64)
+        self.num_flips = np.zeros(graph.n, np.int64)
+        # part_sum starts at the initial assignment (grid_chain_sec11.py:219)
+        self.part_sum = self.label_value[np.asarray(init_labels, np.int64)].copy()
+        self.last_flipped = np.zeros(graph.n, np.int64)
+        self._s = _OrcMaps(_ptr(self.cut_times), _ptr(self.num_flips), _ptr(self.part_sum),
+                           _ptr(self.last_flipped), _ptr(self.label_value), -1, 0)
+
+    @property
+    def cur_f(self):
+        return self._s.cur_f
+
+    def finalized_part_sum(self, labels, n_yields):
+        """grid_chain_sec11.py:416-419: never-flipped nodes get t * final label."""
+        ps = self.part_sum.copy()
+        never = self.last_flipped == 0
+        ps[never] = n_yields * self.label_value[np.asarray(labels, np.int64)[never]]
+        return ps
+
+
 def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps,
-              max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False):
+              max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False,
+              maps=None):
     """Run one chain on the CPU oracle.  ``graph`` needs rowptr/col/pop/n/grid_w.
 
     Returns (labels, stats, pops, trace-or-None); ``labels`` is a new int16 array.
+    ``maps`` (an oracle ``Maps``) accumulates the per-yield spatial observables.
     """
     lab = np.array(labels, dtype=np.int16, copy=True)
     st = new_stats(1) if stats is None else stats
     thr = np.ascontiguousarray(thr, dtype=np.float64)
     tr = np.full(int(steps), -2, dtype=np.int32) if trace else None
     pops = np.zeros(k, dtype=np.int64)
-    rc = lib().orc_run_chain(
+    rc = lib().orc_run_chain_maps(
         _ptr(graph.rowptr), _ptr(graph.col), _ptr(graph.pop), graph.n, graph.grid_w, k, mode,
         int(pop_lo), int(pop_hi), _ptr(thr), int(seed), int(chain_id), _ptr(lab), _ptr(st),
         int(steps), int(max_retries), _ptr(hist_cut), _ptr(hist_b), _ptr(tr), _ptr(pops),
+        None if maps is None else ctypes.byref(maps._s),
     )
     if rc != 0:
         raise MemoryError("oracle allocation failed")

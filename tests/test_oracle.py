@@ -158,3 +158,39 @@ def test_stuck_instead_of_infinite_loop():
     out, st, _, _ = O.run_chain(g, lab, 2, 0, 18, 18, thr, 0, 0, 10, max_retries=50)
     assert st["stuck"][0] == 1 and st["steps"][0] == 0 and st["attempts"][0] == 50
     assert np.array_equal(out, lab)
+
+
+@pytest.mark.parametrize("name", ["grid10_k2_bi", "grid12_k4_pairs", "grid7x9_k3_cut",
+                                  "sec11_a2_k2"])
+def test_oracle_maps_follow_the_reference_driver(name):
+    """orc maps == a literal replay of grid_chain_sec11.py:383-384,396-400 over the trace."""
+    case = CASES[name]
+    g = case.graph
+    lo, hi = case.bounds
+    vals = np.array([-1, 1] if case.k == 2 else [5 - 2 * d for d in range(case.k)], np.int64)
+    S = 250
+    M = O.Maps(g, case.init, vals)
+    O.run_chain(g, case.init, case.k, case.mode, lo, hi, case.thr, 3, 1, S, maps=M)
+    e = g.edges()
+    lab, st = case.init.copy(), O.new_stats(1)
+    ct = np.zeros(len(e), np.int64)
+    nf = np.zeros(g.n, np.int64)
+    lf = np.zeros(g.n, np.int64)
+    ps = vals[case.init.astype(np.int64)].copy()
+    f = None
+    for t in range(S + 1):  # yield t: the initial state, then one state per counted step
+        if t > 0:
+            prev = lab
+            lab, st, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, case.thr, 3, 1, 1,
+                                        stats=st)
+            changed = np.flatnonzero(prev != lab)
+            if len(changed):
+                f = int(changed[0])
+        cur = lab.astype(np.int64)
+        ct += cur[e[:, 0]] != cur[e[:, 1]]
+        if f is not None:  # part.flips is not None
+            ps[f] -= vals[cur[f]] * (t - lf[f])
+            lf[f] = t
+            nf[f] += 1
+    assert np.array_equal(ct, M.cut_times) and np.array_equal(nf, M.num_flips)
+    assert np.array_equal(ps, M.part_sum) and np.array_equal(lf, M.last_flipped)
