@@ -156,6 +156,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--maps", action="store_true",
+                    help="also keep the spatial observables (cut_times, part_sum, ...) per chain")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
                     help="per-launch HBM bytes from a rocprofv3 PMC pass of the default C3 "
                          "command (scripts/profile.sh -> scripts/pmc_summary.py)")
@@ -191,6 +193,8 @@ def main():
     dg = DeviceGraph(g, device=local_rank)
     ch = Chains(dg, chains, k, init, proposal=proposal, pop_bounds=bounds, base=base,
                 seed=args.seed, chain_id0=cid0)
+    if args.maps:
+        ch.enable_maps([-1, 1] if k == 2 else None)
 
     def barrier():
         torch.cuda.synchronize(local_rank)
@@ -251,6 +255,7 @@ def main():
                 "workload": f"{desc}, {chains} chains/GPU, {proposal} proposal, {base_desc}, "
                             f"{percent:.0%} pop bound, contiguity",
                 "chains_per_gpu": chains,
+                "spatial_maps": bool(args.maps),
                 "flip_steps_per_chain_per_step": args.inner,
                 "parallelism": f"chains sharded over {world} GPU(s), RCCL histogram merge",
             },

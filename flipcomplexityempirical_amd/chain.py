@@ -231,29 +231,41 @@ class RunResult:
     hist_b: np.ndarray      # yields per |B|
     pops: np.ndarray        # [n_chains, k]
     kernel_ms: float
+    maps: Optional[dict] = None  # spatial observables (Chains.read_map), per chain
 
     def expected_wait_sums(self, n_nodes: int, k: int) -> np.ndarray:
         return expected_wait_sum(self.stats, n_nodes, k)
 
 
+def read_maps(ch: "Chains", finalize: bool = True) -> dict:
+    """All four spatial maps of every chain; part_sum finalised as the reference's
+    end-of-run loop does (grid_chain_sec11.py:416-419) unless ``finalize`` is False."""
+    return {"cut_times": ch.read_map("cut_times"), "num_flips": ch.read_map("num_flips"),
+            "part_sum": ch.read_map("part_sum", finalize=finalize),
+            "last_flipped": ch.read_map("last_flipped")}
+
+
 def run_chains(graph: Graph, init_labels, k: int, n_chains: int, steps: int,
                proposal: str | int = "pairs", percent: float = 0.05, base=1.0, seed: int = 0,
                chain_id0: int = 0, device: int = 0, pop_bounds=None,
-               max_retries: int = DEFAULT_MAX_RETRIES, total_steps: Optional[int] = None
-               ) -> RunResult:
+               max_retries: int = DEFAULT_MAX_RETRIES, total_steps: Optional[int] = None,
+               maps: bool = False, label_values=None) -> RunResult:
     """Run ``n_chains`` chains for ``steps`` counted steps each and read everything back.
 
     ``total_steps`` (GerryChain's meaning: yields including the initial state) may be
-    given instead of ``steps``; then steps = total_steps - 1.
+    given instead of ``steps``; then steps = total_steps - 1.  ``maps`` also returns the
+    driver's spatial observables (``label_values``: GerryChain values of districts 0..k-1).
     """
     if total_steps is not None:
         steps = int(total_steps) - 1
     dg = DeviceGraph(graph, device)
     ch = Chains(dg, n_chains, k, init_labels, proposal=proposal, pop_bounds=pop_bounds,
                 percent=percent, base=base, seed=seed, chain_id0=chain_id0)
+    if maps:
+        ch.enable_maps(label_values)
     ch.run(steps, max_retries)
     res = RunResult(ch.labels(), ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(),
-                    ch.last_kernel_ms())
+                    ch.last_kernel_ms(), read_maps(ch) if maps else None)
     ch.close()
     dg.close()
     return res

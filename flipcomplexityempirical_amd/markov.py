@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _lib
 from .chain import (DEFAULT_MAX_RETRIES, Chains, DeviceGraph, RunResult, eval_flips,
-                    population_bounds)
+                    population_bounds, read_maps)
 from .graph import Graph
 
 
@@ -144,6 +144,35 @@ def geom_wait(partition: Partition):
     """grid_chain_sec11.py:147-148 (numpy geometric draw, as the reference)."""
     p = len(list(partition["b_nodes"])) / (len(partition.graph.nodes) ** len(partition.parts) - 1)
     return int(np.random.geometric(p, 1)) - 1
+
+
+def boundary_slope(partition: Partition, last: int = 39):
+    """grid_chain_sec11.py:55-78 ("slope" updater): the cut edges that lie on the outer
+    ring of the sec11 grid (both endpoints in row 0, column 0, row 39 or column 39) or
+    are one of its four corner diagonals, as a list (of a set, as the reference)."""
+    diag = {((0, 1), (1, 0)), ((0, last - 1), (1, last)), ((last - 1, 0), (last, 1)),
+            ((last - 1, last), (last, last - 1))}
+    diag |= {(b, a) for a, b in diag}
+    out = set()
+    for x in partition["cut_edges"]:
+        if (x[0][0] == 0 and x[1][0] == 0) or (x[0][1] == 0 and x[1][1] == 0) or \
+                (x[0][0] == last and x[1][0] == last) or (x[0][1] == last and x[1][1] == last) or \
+                x in diag:
+            out.add(x)
+    return list(out)
+
+
+def slope_and_angle(temp, centre=(20, 20)):
+    """grid_chain_sec11.py:371-394: slope between the midpoints of the first two ring cut
+    edges, and the angle they subtend at the grid centre (np.inf for a vertical pair)."""
+    enda = ((temp[0][0][0] + temp[0][1][0]) / 2, (temp[0][0][1] + temp[0][1][1]) / 2)
+    endb = ((temp[1][0][0] + temp[1][1][0]) / 2, (temp[1][0][1] + temp[1][1][1]) / 2)
+    slope = (endb[1] - enda[1]) / (endb[0] - enda[0]) if endb[0] != enda[0] else np.inf
+    anga = np.array((enda[0] - centre[0], enda[1] - centre[1]))
+    angb = np.array((endb[0] - centre[0], endb[1] - centre[1]))
+    angle = np.arccos(np.clip(np.dot(anga / np.linalg.norm(anga), angb / np.linalg.norm(angb)),
+                              -1, 1))
+    return slope, angle
 
 
 # ===================================================================== proposals
@@ -345,11 +374,18 @@ class MarkovChain:
     def __len__(self):
         return self.total_steps
 
-    def run_batched(self, n_chains: int, chain_id0: int = 0) -> RunResult:
-        """n_chains independent copies for total_steps yields each (no per-state objects)."""
+    def run_batched(self, n_chains: int, chain_id0: int = 0, maps: bool = False) -> RunResult:
+        """n_chains independent copies for total_steps yields each (no per-state objects).
+
+        ``maps`` adds the driver's spatial observables per chain, keyed by node / edge
+        index (grid_chain_sec11.py:383-400, finalised as :416-419), with the initial
+        partition's own label values (e.g. -1/+1) in part_sum.
+        """
         ch = self._make(n_chains, chain_id0)
+        if maps:
+            ch.enable_maps(np.asarray(self.initial_state._label_values, np.int64))
         ch.run(self.total_steps - 1, self.max_retries)
         res = RunResult(ch.labels(), ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(),
-                        ch.last_kernel_ms())
+                        ch.last_kernel_ms(), read_maps(ch) if maps else None)
         ch.close()
         return res

@@ -92,3 +92,59 @@ def test_run_batched_matches_oracle(gpu_lib):
         olab, _, _, _ = O.run_chain(g, sec11_seed(g, 0), 2, 0, lo, hi, metropolis_table(MU, 4), 9,
                                     100 + i, 1000)
         assert np.array_equal(res.labels[i], olab)
+
+
+def test_boundary_slope_updater_on_host():
+    """A15 (grid_chain_sec11.py:55-78, 371-394) through the façade's host updaters."""
+    g, part = sec11_partition(alignment=0)  # rows >= 20 vs rows < 20: a horizontal cut
+    part.updaters["slope"] = gc.boundary_slope
+    temp = part["slope"]
+    assert sorted(temp) == sorted([((19, 0), (20, 0)), ((19, 39), (20, 39))])
+    slope, angle = gc.slope_and_angle(temp)
+    assert slope == np.inf and np.isclose(angle, np.pi, atol=0.06)  # midpoints share row 19.5
+
+
+@pytest.mark.gpu
+def test_reference_driver_loop_matches_gpu_maps(gpu_lib):
+    """grid_chain_sec11.py:366-419 run literally over the façade's yielded partitions
+    (cut_times per edge, part_sum / last_flipped / num_flips per node, slope and angle)
+    equals the GPU's spatial maps of the same chain (MarkovChain.run_batched(maps=True))."""
+    g, part = sec11_partition(alignment=2, base=0.1)
+    part.updaters["slope"] = gc.boundary_slope
+    pb = gc.within_percent_of_ideal_population(part, 0.05)
+    mk = lambda: gc.MarkovChain(gc.slow_reversible_propose_bi,  # noqa: E731
+                                gc.Validator([gc.single_flip_contiguous, pb]),
+                                accept=gc.cut_accept, initial_state=part, total_steps=1200,
+                                seed=4, chain_id=0, chunk=500)
+    idx = g.index()
+    eid = {tuple(e): i for i, e in enumerate(g.edges().tolist())}
+    cut_times = np.zeros(g.n_edges, np.int64)
+    part_sum = np.array([part.assignment[x] for x in g.nodes], np.int64)
+    last_flipped = np.zeros(g.n, np.int64)
+    num_flips = np.zeros(g.n, np.int64)
+    slopes, angles = [], []
+    t = 0
+    for p in mk():
+        for a, b in p["cut_edges"]:
+            i, j = idx[a], idx[b]
+            cut_times[eid[(min(i, j), max(i, j))]] += 1
+        temp = p["slope"]
+        if len(temp) >= 2:
+            s_, a_ = gc.slope_and_angle(temp)
+            slopes.append(s_)
+            angles.append(a_)
+        if p.flips is not None:
+            f = idx[list(p.flips.keys())[0]]
+            part_sum[f] -= p.assignment[g.nodes[f]] * (t - last_flipped[f])
+            last_flipped[f] = t
+            num_flips[f] += 1
+        t += 1
+    final = p
+    never = last_flipped == 0
+    part_sum[never] = t * np.array([final.assignment[g.nodes[x]] for x in np.flatnonzero(never)])
+    res = mk().run_batched(1, chain_id0=0, maps=True)
+    assert np.array_equal(res.maps["cut_times"][0], cut_times)
+    assert np.array_equal(res.maps["num_flips"][0], num_flips)
+    assert np.array_equal(res.maps["last_flipped"][0], last_flipped)
+    assert np.array_equal(res.maps["part_sum"][0], part_sum)
+    assert len(slopes) == t and np.all(np.isfinite(angles))
