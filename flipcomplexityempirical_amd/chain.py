@@ -47,6 +47,17 @@ def metropolis_table(base: float, maxdeg: int) -> np.ndarray:
     return np.array([b ** (-d) for d in range(-maxdeg, maxdeg + 1)], dtype=np.float64)
 
 
+def annealing_table(base: float, beta: float, maxdeg: int) -> np.ndarray:
+    """thr[d + maxdeg] = base ** (beta * (-d)): the power of annealing_cut_accept_backwards
+    (grid_chain_sec11.py:101), base**(beta*(-len(cut)+len(parent cut))), for Δcut = d."""
+    b = float(base)
+    return np.array([b ** (beta * (-d)) for d in range(-maxdeg, maxdeg + 1)], dtype=np.float64)
+
+
+ACCEPT_RULES = {"cut": _lib.ACCEPT_CUT, "bratio": _lib.ACCEPT_BRATIO,
+                "boundary": _lib.ACCEPT_BOUNDARY}
+
+
 def expected_wait_sum(stats, n_nodes: int, k: int) -> np.ndarray:
     """Σ_t E[geom_wait_t] = (N^k - 1) * Σ 1/|B_t| - T (geom_wait, grid_chain_sec11.py:147-148)."""
     M = float(n_nodes ** k - 1)
@@ -92,7 +103,8 @@ class Chains:
 
     def __init__(self, dgraph: DeviceGraph, n_chains: int, k: int, init_labels,
                  proposal: str | int = "pairs", pop_bounds=None, percent: float = 0.05,
-                 base: float | Sequence[float] = 1.0, seed: int = 0, chain_id0: int = 0):
+                 base: float | Sequence[float] = 1.0, seed: int = 0, chain_id0: int = 0,
+                 thr: Optional[np.ndarray] = None):
         L = _lib.require_device()
         self.dgraph = dgraph
         g = dgraph.graph
@@ -106,7 +118,10 @@ class Chains:
             pop_bounds = population_bounds(g.total_pop, k, percent)
         self.pop_lo, self.pop_hi = int(pop_bounds[0]), int(pop_bounds[1])
         D = dgraph.maxdeg
-        if np.ndim(base) == 0:
+        if thr is not None:  # an explicit bound table [2*maxdeg+1] or [n_chains][2*maxdeg+1]
+            thr = np.asarray(thr, np.float64)
+            thr_per = 1 if thr.ndim == 2 else 0
+        elif np.ndim(base) == 0:
             thr = metropolis_table(float(base), D)
             thr_per = 0
         else:
@@ -164,6 +179,14 @@ class Chains:
 
     def pops(self) -> np.ndarray:
         return self._read(_lib.READ_POPS, np.empty((self.n_chains, self.k), np.int64))
+
+    def set_accept(self, rule: str | int, node_flags=None) -> None:
+        """Accept rule: "cut" (cut_accept), "bratio" (annealing_cut_accept_backwards' |B'|/|B|
+        factor on the tabulated power) or "boundary" (uniform_accept + boundary_condition
+        over ``node_flags``, the boundary_node attribute); see include/flipwalk.h."""
+        r = ACCEPT_RULES[rule] if isinstance(rule, str) else int(rule)
+        fl = None if node_flags is None else np.ascontiguousarray(node_flags, np.uint8)
+        check(_lib.load().fw_chains_set_accept(self._h, r, ptr(fl)))
 
     # ------------------------------------------------------------- spatial maps
     def enable_maps(self, label_values: Optional[Sequence[int]] = None) -> None:

@@ -126,6 +126,9 @@ struct fw_chains {
   int64_t* d_ps = nullptr;
   int32_t* d_pend = nullptr;
   int64_t* d_labval = nullptr;
+  // FW_ACCEPT_BOUNDARY
+  uint8_t* d_flags = nullptr;
+  int32_t* d_bcnt = nullptr;
 };
 
 namespace {
@@ -333,7 +336,7 @@ void fw_chains_destroy(fw_chains* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr,  c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
-                  c->d_pend,   c->d_labval};
+                  c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -613,6 +616,35 @@ int fw_chains_reset_observables(fw_chains* c) {
       return fail(FW_EHIP, "map re-init failed");
     c->max_yields = 0;
   }
+  return FW_OK;
+}
+
+int fw_chains_set_accept(fw_chains* c, int32_t rule, const uint8_t* node_flags) {
+  if (!c) return fail(FW_EINVAL, "null handle");
+  if (rule < FW_ACCEPT_CUT || rule > FW_ACCEPT_BOUNDARY)
+    return fail(FW_EINVAL, "unknown accept rule %d", rule);
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (rule == FW_ACCEPT_BOUNDARY) {
+    if (!node_flags) return fail(FW_EINVAL, "FW_ACCEPT_BOUNDARY needs node flags");
+    const int n = c->g->n;
+    int nflag = 0;
+    for (int x = 0; x < n; ++x) nflag += node_flags[x] ? 1 : 0;
+    if (nflag == 0)  // boundary_condition reads blist[0] (grid_chain_sec11.py:46)
+      return fail(FW_EINVAL, "boundary_condition needs at least one boundary_node");
+    const size_t nb = sizeof(int32_t) * (size_t)c->n_chains * c->k;
+    if (!c->d_flags) {
+      if (hipMalloc(&c->d_flags, n) != hipSuccess || hipMalloc(&c->d_bcnt, nb) != hipSuccess)
+        return fail(FW_ENOMEM, "flag buffers");
+    }
+    HIPCHK(hipMemcpy(c->d_flags, node_flags, n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(c->d_bcnt, 0, nb));
+    c->p.flags = c->d_flags;
+    c->p.bcnt = c->d_bcnt;
+    if (fw_launch_bcnt_init(c->p, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess)
+      return fail(FW_EHIP, "flag count init failed");
+  }
+  c->p.accept = rule;
   return FW_OK;
 }
 

@@ -400,6 +400,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     uint32_t n_yield = 0, retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
     Pend pend = pend_load(p, cc);
+    // boundary_node-flagged nodes of district q (FW_ACCEPT_BOUNDARY), lane q
+    int32_t bcnt = p.accept == FW_ACCEPT_BOUNDARY && q < k ? p.bcnt[(size_t)cc * k + q] : 0;
     lds_order();
 
     // ---- derive group sums, cut / boundary / proposal-set counts (per row)
@@ -704,26 +706,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         else if (!contig) n_conf += 1;
         retries = valid ? 0u : retries + 1u;
       }
-      // Metropolis (cut_accept, grid_chain_sec11.py:171-179): lane dcut+D holds the bound
-      const bool acc_l = u53(x.x2, x.x3) < thr_l;
-      const bool accepted = valid && ((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u);
-      if (valid && p.trace && q == 0)
-        p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
-      n_steps += valid ? 1u : 0u;
-      if (p.m_acc != nullptr && accepted) {  // spatial observables: fire-and-forget atomics
-        const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
-        if (q >= 1 && q <= 4 && h.x >= 0 && (h.lx == a || h.lx == d)) {
-          const int e = q == 1   ? grid_eid_down(vr - 1, vc, W, H)
-                        : q == 2 ? grid_eid_right(vr, vc - 1, W, H)
-                        : q == 3 ? grid_eid_right(vr, vc, W, H)
-                                 : grid_eid_down(vr, vc, W, H);
-          map_edge(p, c, e, h.lx == a, t);
-        }
-        if (q == 0) map_run_end(p, c, pend, t);
-        pend = Pend{v, (int32_t)d, (uint32_t)t};
-      }
-
-      // ---- commit (accepting rows)
+      // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
       uint32_t wo = 0, wn = 0;
       const bool mine = q <= 4 && h.x >= 0;
       if (mine) {
@@ -744,6 +727,41 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           wn = (uint32_t)__popc((h.bits | (h.has_v ? 1u << d : 0u)) & keep);
         }
       }
+      const uint64_t b_plus = ballot(valid && mine && wo == 0 && wn > 0);
+      const uint64_t b_minus = ballot(valid && mine && wo > 0 && wn == 0);
+      const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
+      // ---- accept rule (lane dcut+D holds the tabulated bound; include/flipwalk.h)
+      bool accepted;
+      if (p.accept == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
+        const int32_t fv = p.flags[v] ? 1 : 0;
+        const int32_t cnt = bcnt - ((uint32_t)q == a ? fv : 0) + ((uint32_t)q == d ? fv : 0);
+        accepted = valid && __popc(rowbits(ballot(q < k && cnt > 0), row)) >= 2;
+      } else {
+        // cut_accept (grid_chain_sec11.py:171-179), or with the |B'|/|B| factor of
+        // annealing_cut_accept_backwards (:81-110)
+        const double bound = p.accept == FW_ACCEPT_BRATIO
+                                 ? thr_l * ((double)(bnodes + plus - minus) / (double)bnodes)
+                                 : thr_l;
+        const bool acc_l = u53(x.x2, x.x3) < bound;
+        accepted = valid && ((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u);
+      }
+      if (valid && p.trace && q == 0)
+        p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
+      n_steps += valid ? 1u : 0u;
+      if (p.m_acc != nullptr && accepted) {  // spatial observables: fire-and-forget atomics
+        const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
+        if (q >= 1 && q <= 4 && h.x >= 0 && (h.lx == a || h.lx == d)) {
+          const int e = q == 1   ? grid_eid_down(vr - 1, vc, W, H)
+                        : q == 2 ? grid_eid_right(vr, vc - 1, W, H)
+                        : q == 3 ? grid_eid_right(vr, vc, W, H)
+                                 : grid_eid_down(vr, vc, W, H);
+          map_edge(p, c, e, h.lx == a, t);
+        }
+        if (q == 0) map_run_end(p, c, pend, t);
+        pend = Pend{v, (int32_t)d, (uint32_t)t};
+      }
+
+      // ---- commit (accepting rows)
       if (accepted) {
         if (q == 0) P::axor(lab, v, a ^ d);
         // u16 group sum inside its u32 pair: a wrapping 32-bit add of the shifted
@@ -752,9 +770,6 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           lds_add(gsum + (h.x >> 7), (wn - wo) << (16 * ((h.x >> 6) & 1)));
       }
       lds_order();
-      const uint64_t b_plus = ballot(accepted && mine && wo == 0 && wn > 0);
-      const uint64_t b_minus = ballot(accepted && mine && wo > 0 && wn == 0);
-      const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
       const int dnp = (int)row_sum(accepted && mine ? wn - wo : 0u);
       if (accepted) {
         n_acc += 1;
@@ -766,6 +781,10 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (plus | minus) invb = 1.0 / (double)bnodes;
         if ((uint32_t)q == a) pops -= pv;
         if ((uint32_t)q == d) pops += pv;
+        if (p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
+          if ((uint32_t)q == a) bcnt -= 1;
+          if ((uint32_t)q == d) bcnt += 1;
+        }
       }
       observe(valid);
       STAMP(5);  // outcome, Metropolis, commit, observe
@@ -782,6 +801,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
       if (q < k) p.pops[(size_t)c * k + q] = pops;
+      if (q < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
       if (q == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
       if (q == 0) {
         stp->attempts = attempts;

@@ -63,6 +63,11 @@ struct FwRunParams {
   int64_t* m_ps;
   int32_t* m_pend;
   const int64_t* m_labval;     // [k] GerryChain label values
+  // accept rule (FW_ACCEPT_*); FW_ACCEPT_BOUNDARY: node flags and, per chain, the count
+  // of flagged nodes in each district [n_chains][k]
+  int32_t accept;
+  const uint8_t* flags;
+  int32_t* bcnt;
 };
 
 // fw_chains_read_map: finalise maps of a chain range (see include/flipwalk.h)
@@ -104,6 +109,7 @@ struct FwEvalParams {
 // Host-side launchers implemented in fw_kernels.hip.
 int fw_launch_map_init(const FwRunParams& p, void* stream);
 int fw_launch_map_read(const FwMapRead& m, void* stream);
+int fw_launch_bcnt_init(const FwRunParams& p, void* stream);
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);

@@ -77,6 +77,8 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
     uint32_t n_sdeg = 0, n_adeg = 0, n_bchg = 0, n_yield = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
     Pend pend = pend_load(p, c);
+    // boundary_node-flagged nodes of district `lane` (FW_ACCEPT_BOUNDARY)
+    int32_t bcnt = p.accept == FW_ACCEPT_BOUNDARY && lane < k ? p.bcnt[(size_t)c * k + lane] : 0;
     __syncthreads();
 
     // ---- derive group sums, cut count, boundary count, proposal-set size
@@ -199,8 +201,24 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       }
       if (!valid) break;
       n_steps += 1;
-      // ---- Metropolis (cut_accept, grid_chain_sec11.py:171-179)
-      const bool accepted = u53(x.x2, x.x3) < rdl_f64(thr_l, dcut + D);
+      // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
+      uint32_t wo, wn;
+      C.template weights_old_new<MODE>(h, a, d, m, nbd, wo, wn);
+      const bool mine = GRID ? lane <= 4 : lane <= dv;
+      const int plus = __popcll(ballot(mine && wo == 0 && wn > 0));
+      const int minus = __popcll(ballot(mine && wo > 0 && wn == 0));
+      // ---- accept rule (include/flipwalk.h FW_ACCEPT_*)
+      bool accepted;
+      if (p.accept == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
+        const int32_t fv = p.flags[v] ? 1 : 0;
+        const int32_t cnt = bcnt - (lane == (int)a ? fv : 0) + (lane == (int)d ? fv : 0);
+        accepted = __popcll(ballot(lane < k && cnt > 0)) >= 2;
+      } else {  // cut_accept (grid_chain_sec11.py:171-179) [* |B'|/|B|, :81-110]
+        double bound = rdl_f64(thr_l, dcut + D);
+        if (p.accept == FW_ACCEPT_BRATIO)
+          bound = bound * ((double)(bnodes + plus - minus) / (double)bnodes);
+        accepted = u53(x.x2, x.x3) < bound;
+      }
       if (p.trace && lane == 0) p.trace[(size_t)c * p.steps + s] = accepted ? v * 64 + (int)d : -1;
       if (accepted && p.m_acc != nullptr) {  // spatial observables: fire-and-forget atomics
         const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
@@ -226,14 +244,9 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       if (accepted) {
         n_acc += 1;
         n_adeg += (uint32_t)dv;
-        uint32_t wo, wn;
-        C.template weights_old_new<MODE>(h, a, d, m, nbd, wo, wn);
-        const bool mine = GRID ? lane <= 4 : lane <= dv;
         if (lane == 0) PK<LB>::axor(C.lab, v, a ^ d);
         if (mine && h.x >= 0 && wn != wo) lds_add(C.gsum + (h.x >> 6), wn - wo);
         lds_order();
-        const int plus = __popcll(ballot(mine && wo == 0 && wn > 0));
-        const int minus = __popcll(ballot(mine && wo > 0 && wn == 0));
         npairs += (int32_t)wave_sum(mine ? wn - wo : 0u);
         cut += dcut;
         bnodes += plus - minus;
@@ -241,6 +254,10 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
         if (plus | minus) invb = 1.0 / (double)bnodes;
         if (lane == (int)a) pops -= pv;
         if (lane == (int)d) pops += pv;
+        if (p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
+          if (lane == (int)a) bcnt -= 1;
+          if (lane == (int)d) bcnt += 1;
+        }
       }
       observe();
     }
@@ -253,6 +270,7 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(C.lab);
       for (int i = lane; i < p.lab_bytes / 16; i += WAVE) dst[i] = src[i];
       if (lane < k) p.pops[(size_t)c * k + lane] = pops;
+      if (lane < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lane] = bcnt;
     }
     if (lane == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
     if (lane == 0) {
@@ -436,6 +454,22 @@ int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   void* args[] = {const_cast<FwRunParams*>(&p)};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes, (hipStream_t)stream);
   return e == hipSuccess ? 0 : -1;
+}
+
+// flagged nodes per district of every chain's current plan (FW_ACCEPT_BOUNDARY)
+__global__ void fw_bcnt_init_kernel(FwRunParams p, int lb) {
+  const size_t total = (size_t)p.n_chains * (size_t)p.g.n;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t c = i / (size_t)p.g.n;
+    const int x = (int)(i - c * (size_t)p.g.n);
+    if (p.flags[x]) atomicAdd(p.bcnt + c * p.k + glabel(p.labels + c * p.lab_stride, lb, x), 1);
+  }
+}
+
+int fw_launch_bcnt_init(const FwRunParams& p, void* stream) {
+  hipLaunchKernelGGL(fw_bcnt_init_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, p, p.lb);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int fw_launch_map_init(const FwRunParams& p, void* stream) {

@@ -66,6 +66,20 @@ extern "C" {
 #define FW_PROPOSE_PAIRS 1
 #define FW_PROPOSE_CUTEDGE 2
 
+/* ---- accept rules (fw_chains_set_accept) --------------------------------------
+ * FW_ACCEPT_CUT      cut_accept grid_chain_sec11.py:171-179 (the default):
+ *                    accept iff u < thr[Δcut + maxdeg]  (thr[d] = base**(-d))
+ * FW_ACCEPT_BRATIO   annealing_cut_accept_backwards grid_chain_sec11.py:81-110:
+ *                    accept iff u < thr[Δcut + maxdeg] * (|B'| / |B|), |B| = boundary
+ *                    nodes (b_nodes_bi) before / after the flip; the host tabulates
+ *                    thr[d] = base**(beta*(-d)) (the reference: base .1, beta 5)
+ * FW_ACCEPT_BOUNDARY uniform_accept + boundary_condition :43-52,159-165: accept iff
+ *                    the nodes flagged boundary_node span >= 2 districts after the flip
+ * (u = the CPython random() draw of the attempt, include/flipwalk.h header.)        */
+#define FW_ACCEPT_CUT 0
+#define FW_ACCEPT_BRATIO 1
+#define FW_ACCEPT_BOUNDARY 2
+
 /* ---- what fw_chains_read can return -------------------------------------- */
 #define FW_READ_LABELS 0   /* int16  [n_chains][n]                            */
 #define FW_READ_STATS 1    /* fw_chain_stats [n_chains]                       */
@@ -177,6 +191,11 @@ int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes);
 
 /* Zero the per-chain sums and the yield histograms (not the chain states). */
 int fw_chains_reset_observables(fw_chains* c);
+
+/* Select the accept rule (FW_ACCEPT_*) for every chain; node_flags [n] (1 =
+ * boundary_node) is required by FW_ACCEPT_BOUNDARY and ignored otherwise.  May be
+ * called between runs. */
+int fw_chains_set_accept(fw_chains* c, int32_t rule, const uint8_t* node_flags);
 
 /* Turn on the spatial observables for every chain (before the first run).
  * label_values [k] are the GerryChain assignment values of districts 0..k-1

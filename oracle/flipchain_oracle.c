@@ -111,6 +111,9 @@ typedef struct {
   uint64_t* hist_cut; /* may be NULL */
   uint64_t* hist_b;   /* may be NULL */
   struct orc_maps* maps; /* may be NULL */
+  int32_t accept_rule;   /* FW_ACCEPT_* */
+  const uint8_t* flags;  /* [n] boundary_node flags (FW_ACCEPT_BOUNDARY), may be NULL */
+  int64_t* bcnt;         /* [k] flagged nodes per district */
 } chain_t;
 
 /* The reference driver's spatial observables, updated once per yield exactly as
@@ -197,6 +200,53 @@ static void derive(chain_t* c) {
   c->st.cut = (int32_t)(cut2 / 2);
   c->st.bnodes = bn;
   c->st.npairs = (int32_t)np;
+  for (int32_t i = 0; i < c->k; ++i) c->bcnt[i] = 0;
+  if (c->flags)
+    for (int32_t x = 0; x < g->n; ++x) c->bcnt[c->lab[x]] += c->flags[x] ? 1 : 0;
+}
+
+/* |B| after flipping v -> b (b_nodes_bi of the proposed state) */
+static int32_t bnodes_after(chain_t* c, int32_t v, int16_t b) {
+  const graph_t* g = &c->g;
+  const int16_t a = c->lab[v];
+  int32_t before = 0, after = 0;
+  for (int32_t e = g->rowptr[v] - 1; e < g->rowptr[v + 1]; ++e) {
+    const int32_t x = e < g->rowptr[v] ? v : g->col[e];
+    before += c->w[x] > 0;
+  }
+  c->lab[v] = b;
+  for (int32_t e = g->rowptr[v] - 1; e < g->rowptr[v + 1]; ++e) {
+    const int32_t x = e < g->rowptr[v] ? v : g->col[e];
+    after += weight(c, x) > 0;
+  }
+  c->lab[v] = a;
+  return c->st.bnodes + after - before;
+}
+
+/* The accept rule on a valid proposal v -> b with draw u:
+ *   FW_ACCEPT_CUT      cut_accept grid_chain_sec11.py:171-179: u < base**(-dcut)
+ *   FW_ACCEPT_BRATIO   annealing_cut_accept_backwards :81-110: u < base**(beta*(-dcut))
+ *                      * (len(b_nodes') / len(b_nodes)), the power tabulated in thr
+ *   FW_ACCEPT_BOUNDARY uniform_accept + boundary_condition :43-52,159-165: u < 1 iff the
+ *                      boundary_node-flagged nodes of the proposed plan span >= 2
+ *                      districts, else u < 0 */
+static int accept_of(chain_t* c, int32_t v, int16_t b, int32_t dcut, double u) {
+  const int32_t D = c->g.maxdeg;
+  if (c->accept_rule == FW_ACCEPT_BRATIO) {
+    const double ratio = (double)bnodes_after(c, v, b) / (double)c->st.bnodes;
+    return u < c->thr[dcut + D] * ratio;
+  }
+  if (c->accept_rule == FW_ACCEPT_BOUNDARY) {
+    const int64_t fv = c->flags && c->flags[v] ? 1 : 0;
+    const int16_t a = c->lab[v];
+    int32_t parts = 0;
+    for (int32_t q = 0; q < c->k; ++q) {
+      const int64_t cnt = c->bcnt[q] - (q == a ? fv : 0) + (q == b ? fv : 0);
+      parts += cnt > 0;
+    }
+    return u < (parts >= 2 ? 1.0 : 0.0);
+  }
+  return u < c->thr[dcut + D];
 }
 
 /* --- contiguity: exact verdict + the same level-synchronous race search the
@@ -416,6 +466,10 @@ static int32_t commit(chain_t* c, int32_t v, int16_t b, int32_t dcut) {
   c->lab[v] = b;
   c->pops[a] -= popof(g, v);
   c->pops[b] += popof(g, v);
+  if (c->flags && c->flags[v]) {
+    c->bcnt[a] -= 1;
+    c->bcnt[b] += 1;
+  }
   c->st.cut += dcut;
   int32_t nb = 0;
   for (int32_t e = g->rowptr[v] - 1; e < g->rowptr[v + 1]; ++e) {
@@ -459,10 +513,11 @@ static int setup(chain_t* c, const int32_t* rowptr, const int32_t* col, const in
   c->w = (int32_t*)calloc((size_t)n, sizeof(int32_t));
   c->fen = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
   c->pops = (int64_t*)calloc((size_t)k, sizeof(int64_t));
+  c->bcnt = (int64_t*)calloc((size_t)k, sizeof(int64_t));
   c->owner = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
   c->list = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
   c->lab = (int16_t*)malloc(sizeof(int16_t) * (size_t)n);
-  if (!c->w || !c->fen || !c->pops || !c->owner || !c->list || !c->lab) return -1;
+  if (!c->w || !c->fen || !c->pops || !c->bcnt || !c->owner || !c->list || !c->lab) return -1;
   for (int32_t x = 0; x < n; ++x) c->owner[x] = -1;
   return 0;
 }
@@ -471,6 +526,7 @@ static void teardown(chain_t* c) {
   free(c->w);
   free(c->fen);
   free(c->pops);
+  free(c->bcnt);
   free(c->owner);
   free(c->list);
   free(c->lab);
@@ -484,12 +540,12 @@ static void teardown(chain_t* c) {
  * Metropolis draw rejected) — used to replay trajectories in tests.
  * Returns 0, or -1 on allocation failure.
  */
-int orc_run_chain_maps(const int32_t* rowptr, const int32_t* col, const int64_t* pop, int32_t n,
-                       int32_t grid_w, int32_t k, int32_t mode, int64_t pop_lo, int64_t pop_hi,
-                       const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
-                       fw_chain_stats* stats, int64_t steps, int32_t max_retries,
-                       uint64_t* hist_cut, uint64_t* hist_b, int32_t* trace, int64_t* pops_out,
-                       orc_maps* maps) {
+int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* pop, int32_t n,
+                     int32_t grid_w, int32_t k, int32_t mode, int64_t pop_lo, int64_t pop_hi,
+                     const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
+                     fw_chain_stats* stats, int64_t steps, int32_t max_retries,
+                     uint64_t* hist_cut, uint64_t* hist_b, int32_t* trace, int64_t* pops_out,
+                     orc_maps* maps, int32_t accept_rule, const uint8_t* flags) {
   chain_t c;
   if (setup(&c, rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr)) {
     teardown(&c);
@@ -502,9 +558,10 @@ int orc_run_chain_maps(const int32_t* rowptr, const int32_t* col, const int64_t*
   c.hist_cut = hist_cut;
   c.hist_b = hist_b;
   c.maps = maps;
+  c.accept_rule = accept_rule;
+  c.flags = flags;
   derive(&c);
-  const int32_t D = c.g.maxdeg;
-  if (c.st.yields == 0 && c.st.attempts == 0) yield_obs(&c);
+    if (c.st.yields == 0 && c.st.attempts == 0) yield_obs(&c);
   for (int64_t s = 0; s < steps && !c.st.stuck; ++s) {
     int32_t retries = 0;
     int32_t v = -1, dcut = 0;
@@ -546,7 +603,7 @@ int orc_run_chain_maps(const int32_t* rowptr, const int32_t* col, const int64_t*
     if (c.st.stuck) break;
     c.st.steps++;
     double u = orc_u53(x[2], x[3]);
-    int accepted = u < thr[dcut + D];
+    int accepted = accept_of(&c, v, b, dcut, u);
     if (accepted) {
       c.st.accepts++;
       c.st.acc_deg += (uint64_t)(rowptr[v + 1] - rowptr[v]);
@@ -568,9 +625,9 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
                   const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
                   fw_chain_stats* stats, int64_t steps, int32_t max_retries, uint64_t* hist_cut,
                   uint64_t* hist_b, int32_t* trace, int64_t* pops_out) {
-  return orc_run_chain_maps(rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr, seed,
-                            chain_id, labels, stats, steps, max_retries, hist_cut, hist_b, trace,
-                            pops_out, NULL);
+  return orc_run_chain_ex(rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr, seed,
+                          chain_id, labels, stats, steps, max_retries, hist_cut, hist_b, trace,
+                          pops_out, NULL, FW_ACCEPT_CUT, NULL);
 }
 
 /* Per-flip evaluation on one state (the fw_eval_flips contract). */

@@ -65,8 +65,8 @@ def lib():
             ctypes.c_int64, ctypes.c_int32, _P, _P, _P, _P,
         ]
         L.orc_run_chain.restype = ctypes.c_int
-        L.orc_run_chain_maps.argtypes = L.orc_run_chain.argtypes + [_P]
-        L.orc_run_chain_maps.restype = ctypes.c_int
+        L.orc_run_chain_ex.argtypes = L.orc_run_chain.argtypes + [_P, ctypes.c_int32, _P]
+        L.orc_run_chain_ex.restype = ctypes.c_int
         L.orc_eval_flips.argtypes = [
             _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
             ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _P, _P, _P, _P,
@@ -131,22 +131,25 @@ class Maps:
 
 def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps,
               max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False,
-              maps=None):
+              maps=None, accept_rule=0, flags=None):
     """Run one chain on the CPU oracle.  ``graph`` needs rowptr/col/pop/n/grid_w.
 
     Returns (labels, stats, pops, trace-or-None); ``labels`` is a new int16 array.
-    ``maps`` (an oracle ``Maps``) accumulates the per-yield spatial observables.
+    ``maps`` (an oracle ``Maps``) accumulates the per-yield spatial observables;
+    ``accept_rule`` is FW_ACCEPT_* (0 cut_accept, 1 the |B'|/|B| rule, 2 uniform_accept
+    with boundary_condition over the uint8 ``flags``).
     """
+    fl = None if flags is None else np.ascontiguousarray(flags, np.uint8)
     lab = np.array(labels, dtype=np.int16, copy=True)
     st = new_stats(1) if stats is None else stats
     thr = np.ascontiguousarray(thr, dtype=np.float64)
     tr = np.full(int(steps), -2, dtype=np.int32) if trace else None
     pops = np.zeros(k, dtype=np.int64)
-    rc = lib().orc_run_chain_maps(
+    rc = lib().orc_run_chain_ex(
         _ptr(graph.rowptr), _ptr(graph.col), _ptr(graph.pop), graph.n, graph.grid_w, k, mode,
         int(pop_lo), int(pop_hi), _ptr(thr), int(seed), int(chain_id), _ptr(lab), _ptr(st),
         int(steps), int(max_retries), _ptr(hist_cut), _ptr(hist_b), _ptr(tr), _ptr(pops),
-        None if maps is None else ctypes.byref(maps._s),
+        None if maps is None else ctypes.byref(maps._s), int(accept_rule), _ptr(fl),
     )
     if rc != 0:
         raise MemoryError("oracle allocation failed")

@@ -208,12 +208,33 @@ class PopBound:
         return self.lo <= min(vals) and max(vals) <= self.hi
 
 
+# ----------------------------------------------------------------- accept rules
+def annealing_cut_accept_bound(partition, base, beta):
+    """annealing_cut_accept_backwards, grid_chain_sec11.py:81-110 (its bound; the Validator
+    already enforced its inline popbound / single_flip_contiguous checks)."""
+    boundaries1 = {x[0] for x in partition["cut_edges"]}.union(
+        {x[1] for x in partition["cut_edges"]})
+    boundaries2 = {x[0] for x in partition.parent["cut_edges"]}.union(
+        {x[1] for x in partition.parent["cut_edges"]})
+    return (base ** (beta * (-len(partition["cut_edges"]) + len(partition.parent["cut_edges"])))
+            ) * (len(boundaries1) / len(boundaries2))
+
+
+def boundary_condition(partition, blist):
+    """grid_chain_sec11.py:43-52 over blist = partition["boundary"] (boundary_node == 1)."""
+    o_part = partition.assignment[blist[0]]
+    for x in blist:
+        if partition.assignment[x] != o_part:
+            return True
+    return False
+
+
 # ----------------------------------------------------------------- the chain
 class ProxyChain:
     """MarkovChain with cut_accept; yields (state, observables) per counted step."""
 
     def __init__(self, graph_csr, labels, k, mode, percent, base, seed, chain_id,
-                 pop=None):
+                 pop=None, accept="cut", beta=1, flags=None):
         G = nx.Graph()
         n = graph_csr.n
         pops = graph_csr.pop_array() if pop is None else pop
@@ -235,6 +256,8 @@ class ProxyChain:
         self.counters = dict(attempts=0, steps=0, accepts=0, pop_fail=0, contig_fail=0)
         self.obs = dict(yields=0, sum_cut=0, sum_bnodes=0, sum_invb=0.0)
         self.n = n
+        self.accept, self.beta = accept, beta
+        self.blist = None if flags is None else [v for v in range(n) if flags[v]]
 
     def _yield(self):
         s = self.state
@@ -274,7 +297,13 @@ class ProxyChain:
                     continue
                 break
             C["steps"] += 1
-            bound = self.base ** (-len(proposed["cut_edges"]) + len(proposed.parent["cut_edges"]))
+            if self.accept == "bratio":
+                bound = annealing_cut_accept_bound(proposed, self.base, self.beta)
+            elif self.accept == "boundary":  # uniform_accept, grid_chain_sec11.py:159-165
+                bound = 1 if boundary_condition(proposed, self.blist) else 0
+            else:  # cut_accept, grid_chain_sec11.py:171-179
+                bound = self.base ** (-len(proposed["cut_edges"]) +
+                                      len(proposed.parent["cut_edges"]))
             if self.rng.random() < bound:
                 C["accepts"] += 1
                 self.state = proposed

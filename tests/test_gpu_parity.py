@@ -170,3 +170,45 @@ def test_search_list_spill(gpu_lib, name, path, monkeypatch):
     case = {c.name: c for c in CASES}[name]
     st = _run_vs_oracle(case, 21, [400, 400])
     assert (st["bfs_nodes"] > 2 * st["bfs_runs"]).any()  # searches did outgrow the LDS list
+
+
+ACCEPT_CASES = [("grid12_k4_pairs", "bratio", "auto"), ("grid20_k4_mu", "bratio", "wave64"),
+                ("grid16x24_k8", "bratio", "auto"), ("sec11_a2_k2", "bratio", "auto"),
+                ("tract_k4", "bratio", "auto"), ("grid10_k2_bi", "boundary", "auto"),
+                ("grid30x18_k2_bi", "boundary", "wave64"), ("sec11_a0_k2_mu", "boundary", "auto"),
+                ("frank_a2_k2", "boundary", "auto"), ("grid12_k4_cut", "boundary", "auto")]
+
+
+@pytest.mark.parametrize("name,rule,path", ACCEPT_CASES,
+                         ids=[f"{p}-{r}-{n}" for n, r, p in ACCEPT_CASES])
+def test_accept_rules_bit_exact(gpu_lib, name, rule, path, monkeypatch):
+    """annealing_cut_accept_backwards (|B'|/|B| factor, base .1 beta 5) and uniform_accept
+    with boundary_condition (grid_chain_sec11.py:43-52,81-110,159-165) against the oracle."""
+    from flipcomplexityempirical_amd.chain import annealing_table
+    from flipcomplexityempirical_amd.graph import boundary_flags
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    g = case.graph
+    r = 1 if rule == "bratio" else 2
+    thr = annealing_table(0.1, 5, g.maxdeg) if rule == "bratio" else case.thr
+    flags = boundary_flags(g) if rule == "boundary" else None
+    n_chains, seed, id0, steps_list = 9, 77, 40, [600, 900]
+    dg = DeviceGraph(g)
+    ch = Chains(dg, n_chains, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                seed=seed, chain_id0=id0, thr=thr)
+    ch.set_accept(rule, flags)
+    for s in steps_list:
+        ch.run(s)
+    labs, st = ch.labels(), ch.stats()
+    lo, hi = case.bounds
+    for i in range(n_chains):
+        lab, ost = case.init.copy(), O.new_stats(1)
+        for s in steps_list:
+            lab, ost, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, thr, seed, id0 + i, s,
+                                         stats=ost, accept_rule=r, flags=flags)
+        assert np.array_equal(labs[i], lab), (name, i)
+        for f in ("attempts", "steps", "accepts", "sum_cut", "bnodes", "bfs_nodes"):
+            assert st[f][i] == ost[f][0], (name, i, f)

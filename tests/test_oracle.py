@@ -194,3 +194,34 @@ def test_oracle_maps_follow_the_reference_driver(name):
             nf[f] += 1
     assert np.array_equal(ct, M.cut_times) and np.array_equal(nf, M.num_flips)
     assert np.array_equal(ps, M.part_sum) and np.array_equal(lf, M.last_flipped)
+
+
+@pytest.mark.parametrize("name,rule", [("grid10_k2_bi", "bratio"), ("grid12_k4_pairs", "bratio"),
+                                       ("sec11_a2_k2", "bratio"), ("grid10_k2_bi", "boundary"),
+                                       ("sec11_a0_k2_mu", "boundary"),
+                                       ("grid12_k4_cut", "boundary")])
+def test_accept_rules_follow_the_reference_functions(name, rule):
+    """Oracle FW_ACCEPT_BRATIO / FW_ACCEPT_BOUNDARY == the proxy running literal restatements
+    of annealing_cut_accept_backwards (base .1, beta 5 as the reference) and
+    uniform_accept + boundary_condition (grid_chain_sec11.py:43-52,81-110,159-165)."""
+    from flipcomplexityempirical_amd.chain import annealing_table
+    from flipcomplexityempirical_amd.graph import boundary_flags
+    case = CASES[name]
+    g = case.graph
+    S = 300
+    if rule == "bratio":
+        base, beta, flags, r = 0.1, 5, None, 1
+        thr = annealing_table(base, beta, g.maxdeg)
+    else:
+        base, beta, r = case.base, 1, 2
+        flags = boundary_flags(g)
+        thr = case.thr
+    lab, st, _, _ = O.run_chain(g, case.init, case.k, case.mode, *case.bounds, thr, 13, 2, S,
+                                accept_rule=r, flags=flags)
+    ch = ProxyChain(g, case.init, case.k, case.mode, case.percent, base, 13, 2, accept=rule,
+                    beta=beta, flags=flags)
+    ch.run(S, bounds=case.bounds)
+    assert np.array_equal(np.array(ch.labels()), lab)
+    for f in ("attempts", "steps", "accepts"):
+        assert ch.counters[f] == int(st[f][0]), f
+    assert 0 < st["accepts"][0] < S or rule == "boundary"
