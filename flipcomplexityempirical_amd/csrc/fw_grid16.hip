@@ -339,7 +339,9 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
   return verdict == 1;
 }
 
-template <int LB, int MODE, int PER>
+// FULL = false: the lean instantiation for the common configuration (cut_accept, no
+// spatial maps), which then costs no registers for the optional features.
+template <int LB, int MODE, int PER, bool FULL>
 __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
   extern __shared__ __align__(16) uint8_t smem[];
@@ -356,6 +358,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   GLB uint32_t* const spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)n);
   const uint32_t key0 = (uint32_t)p.seed, key1 = (uint32_t)(p.seed >> 32);
   const int GW = (G + 1) >> 1;  // u16-pair words of group sums
+  const bool maps_on = FULL && p.m_acc != nullptr;
+  const int32_t rule = FULL ? p.accept : FW_ACCEPT_CUT;
   int my_dr, my_dc;
   role_off(q <= 8 ? q : 0, my_dr, my_dc);
   auto divmod = [&](int x, int& r, int& c) {
@@ -399,9 +403,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0, n_sdeg = 0, n_adeg = 0, n_bchg = 0;
     uint32_t n_yield = 0, retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
-    Pend pend = pend_load(p, cc);
+    Pend pend = maps_on ? pend_load(p, cc) : Pend{-1, 0, 0u};
     // boundary_node-flagged nodes of district q (FW_ACCEPT_BOUNDARY), lane q
-    int32_t bcnt = p.accept == FW_ACCEPT_BOUNDARY && q < k ? p.bcnt[(size_t)cc * k + q] : 0;
+    int32_t bcnt = rule == FW_ACCEPT_BOUNDARY && q < k ? p.bcnt[(size_t)cc * k + q] : 0;
     lds_order();
 
     // ---- derive group sums, cut / boundary / proposal-set counts (per row)
@@ -732,14 +736,14 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
       // ---- accept rule (lane dcut+D holds the tabulated bound; include/flipwalk.h)
       bool accepted;
-      if (p.accept == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
+      if (rule == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
         const int32_t fv = p.flags[v] ? 1 : 0;
         const int32_t cnt = bcnt - ((uint32_t)q == a ? fv : 0) + ((uint32_t)q == d ? fv : 0);
         accepted = valid && __popc(rowbits(ballot(q < k && cnt > 0), row)) >= 2;
       } else {
         // cut_accept (grid_chain_sec11.py:171-179), or with the |B'|/|B| factor of
         // annealing_cut_accept_backwards (:81-110)
-        const double bound = p.accept == FW_ACCEPT_BRATIO
+        const double bound = rule == FW_ACCEPT_BRATIO
                                  ? thr_l * ((double)(bnodes + plus - minus) / (double)bnodes)
                                  : thr_l;
         const bool acc_l = u53(x.x2, x.x3) < bound;
@@ -748,7 +752,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (valid && p.trace && q == 0)
         p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
       n_steps += valid ? 1u : 0u;
-      if (p.m_acc != nullptr && accepted) {  // spatial observables: fire-and-forget atomics
+      if (maps_on && accepted) {  // spatial observables: fire-and-forget atomics
         const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
         if (q >= 1 && q <= 4 && h.x >= 0 && (h.lx == a || h.lx == d)) {
           const int e = q == 1   ? grid_eid_down(vr - 1, vc, W, H)
@@ -781,7 +785,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (plus | minus) invb = 1.0 / (double)bnodes;
         if ((uint32_t)q == a) pops -= pv;
         if ((uint32_t)q == d) pops += pv;
-        if (p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
+        if (rule == FW_ACCEPT_BOUNDARY && p.flags[v]) {
           if ((uint32_t)q == a) bcnt -= 1;
           if ((uint32_t)q == d) bcnt += 1;
         }
@@ -801,8 +805,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
       if (q < k) p.pops[(size_t)c * k + q] = pops;
-      if (q < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
-      if (q == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
+      if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
+      if (q == 0 && maps_on) pend_store(p, c, pend);
       if (q == 0) {
         stp->attempts = attempts;
         stp->steps += n_steps;
@@ -830,12 +834,20 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   STAMP_FLUSH
 }
 
-template <int LB, int MODE>
+template <int LB, int MODE, bool FULL>
 void* pick16(int G) {
-  if (G <= 16 * 2) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2>);
-  if (G <= 16 * 4) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4>);
-  if (G <= 16 * 10) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10>);
-  return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16>);
+  if (G <= 16 * 2) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL>);
+  if (G <= 16 * 4) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL>);
+  if (G <= 16 * 10) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL>);
+  return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL>);
+}
+
+template <bool FULL>
+void* pick16_mode(const FwRunParams& p) {
+  const bool cut = p.mode == FW_PROPOSE_CUTEDGE;
+  if (p.lb == 2)
+    return cut ? pick16<2, FW_PROPOSE_CUTEDGE, FULL>(p.G) : pick16<2, FW_PROPOSE_PAIRS, FULL>(p.G);
+  return cut ? pick16<4, FW_PROPOSE_CUTEDGE, FULL>(p.G) : pick16<4, FW_PROPOSE_PAIRS, FULL>(p.G);
 }
 
 int round16i(int x) { return (x + 15) / 16 * 16; }
@@ -860,10 +872,8 @@ bool fw_grid16_candidate(int gw, int maxdeg, int G, int k) {
 }
 
 void* fw_grid16_fn(const FwRunParams& p) {
-  const bool cut = p.mode == FW_PROPOSE_CUTEDGE;
-  if (p.lb == 2)
-    return cut ? pick16<2, FW_PROPOSE_CUTEDGE>(p.G) : pick16<2, FW_PROPOSE_PAIRS>(p.G);
-  return cut ? pick16<4, FW_PROPOSE_CUTEDGE>(p.G) : pick16<4, FW_PROPOSE_PAIRS>(p.G);
+  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT;
+  return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
 }
 
 // LDS plan of the grid kernel: per chain slot [labels | u16 group sums], slot stride
@@ -914,7 +924,10 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
 
 int fw_grid16_launch(const FwRunParams& p, int grid, void* stream) {
   void* args[] = {const_cast<FwRunParams*>(&p)};
-  hipError_t e = hipLaunchKernel(fw_grid16_fn(p), dim3(grid), dim3(64 * p.nw), args,
+  void* fn = fw_grid16_fn(p);  // the lean or the FULL instantiation (same LDS plan)
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds16) != hipSuccess)
+    return -1;
+  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * p.nw), args,
                                  (size_t)p.lds16, (hipStream_t)stream);
   return e == hipSuccess ? 0 : -1;
 }
