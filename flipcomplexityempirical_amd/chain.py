@@ -64,6 +64,15 @@ def expected_wait_sum(stats, n_nodes: int, k: int) -> np.ndarray:
     return M * stats["sum_invb"] - stats["yields"].astype(np.float64)
 
 
+def write_wait_txt(path: str, wait_sum: float) -> None:
+    """The reference's only text output (grid_chain_sec11.py:410-411):
+    ``wfile.write(str(sum(waits)))``.  ``wait_sum`` here is the Rao-Blackwellised
+    expectation of the geom_wait sum (expected_wait_sum), written as the nearest integer
+    like the reference's sum of integer draws."""
+    with open(path, "w") as f:
+        f.write(str(int(round(float(wait_sum)))))
+
+
 class DeviceGraph:
     """A CSR graph uploaded to one HIP device (fw_graph)."""
 

@@ -29,9 +29,9 @@ from typing import Any, Callable, Dict, Hashable, Iterable, List, Optional, Sequ
 import numpy as np
 
 from . import _lib
-from .chain import (DEFAULT_MAX_RETRIES, Chains, DeviceGraph, RunResult, eval_flips,
-                    population_bounds, read_maps)
-from .graph import Graph
+from .chain import (DEFAULT_MAX_RETRIES, Chains, DeviceGraph, RunResult, annealing_table,
+                    eval_flips, population_bounds, read_maps)
+from .graph import Graph, boundary_flags
 
 
 # ===================================================================== Partition
@@ -278,6 +278,27 @@ def always_accept(partition: Partition) -> bool:
     return True
 
 
+def annealing_cut_accept_backwards(partition: Partition) -> bool:
+    """grid_chain_sec11.py:81-110 (base .1, beta 5): lowered to FW_ACCEPT_BRATIO."""
+    raise NotImplementedError("annealing_cut_accept_backwards is lowered to the GPU kernel")
+
+
+def uniform_accept(partition: Partition) -> bool:
+    """grid_chain_sec11.py:159-165 (boundary_condition): lowered to FW_ACCEPT_BOUNDARY."""
+    raise NotImplementedError("uniform_accept is lowered to the GPU kernel")
+
+
+class AnnealingCutAccept:
+    """annealing_cut_accept_backwards with explicit base / beta (the reference fixes
+    base = .1, beta = 5): random() < base**(beta*(c_old - c_new)) * |B'| / |B|."""
+
+    def __init__(self, base: float = 0.1, beta: float = 5):
+        self.base, self.beta = float(base), beta
+
+    def __call__(self, partition: Partition) -> bool:
+        raise NotImplementedError("AnnealingCutAccept is lowered to the GPU kernel")
+
+
 class MetropolisCutAccept:
     """cut_accept with an explicit base (no 'base' updater needed)."""
 
@@ -330,8 +351,25 @@ class MarkovChain:
                 "constraints must be [single_flip_contiguous, within_percent_of_ideal_population]")
         lo, hi = bounds[0].bounds
         self.pop_bounds = (int(math.ceil(lo)), int(math.floor(hi)))
+        self.accept_rule, self.thr, self.flags = "cut", None, None
         if isinstance(accept, MetropolisCutAccept):
             self.base = accept.base
+        elif isinstance(accept, AnnealingCutAccept) or \
+                _fname(accept) == "annealing_cut_accept_backwards":
+            a = accept if isinstance(accept, AnnealingCutAccept) else AnnealingCutAccept()
+            self.base, self.accept_rule = a.base, "bratio"
+            self.thr = annealing_table(a.base, a.beta, initial_state.graph.maxdeg)
+        elif _fname(accept) == "uniform_accept":
+            # boundary_condition reads partition["boundary"] (grid_chain_sec11.py:44), the
+            # boundary_node nodes; without that updater the graph's attribute is used
+            self.base, self.accept_rule = 1.0, "boundary"
+            g = initial_state.graph
+            if "boundary" in initial_state.updaters:
+                idx = g.index()
+                self.flags = np.zeros(g.n, np.uint8)
+                self.flags[[idx[x] for x in initial_state["boundary"]]] = 1
+            else:
+                self.flags = boundary_flags(g)
         elif _fname(accept) == "always_accept":
             self.base = 1.0
         elif _fname(accept) == "cut_accept":
@@ -347,9 +385,12 @@ class MarkovChain:
 
     def _make(self, n_chains=1, chain_id0=None) -> Chains:
         dg = _device_graph(self.graph, self.device)
-        return Chains(dg, n_chains, self.k, self.initial_state.labels, proposal=self.mode,
-                      pop_bounds=self.pop_bounds, base=self.base, seed=self.seed,
-                      chain_id0=self.chain_id if chain_id0 is None else chain_id0)
+        ch = Chains(dg, n_chains, self.k, self.initial_state.labels, proposal=self.mode,
+                    pop_bounds=self.pop_bounds, base=self.base, seed=self.seed,
+                    chain_id0=self.chain_id if chain_id0 is None else chain_id0, thr=self.thr)
+        if self.accept_rule != "cut":
+            ch.set_accept(self.accept_rule, self.flags)
+        return ch
 
     def __iter__(self):
         ch = self._make()

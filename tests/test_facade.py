@@ -148,3 +148,30 @@ def test_reference_driver_loop_matches_gpu_maps(gpu_lib):
     assert np.array_equal(res.maps["last_flipped"][0], last_flipped)
     assert np.array_equal(res.maps["part_sum"][0], part_sum)
     assert len(slopes) == t and np.all(np.isfinite(angles))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("accept", ["annealing", "uniform"])
+def test_alternative_accepts_through_the_facade(gpu_lib, accept):
+    """annealing_cut_accept_backwards / uniform_accept (grid_chain_sec11.py:81-110,159-165)
+    recognised by name, lowered to FW_ACCEPT_BRATIO / FW_ACCEPT_BOUNDARY, equal to the
+    oracle; uniform_accept takes the nodes of the partition's "boundary" updater."""
+    from flipcomplexityempirical_amd.chain import annealing_table
+    from flipcomplexityempirical_amd.graph import boundary_flags
+    g, part = sec11_partition(alignment=1, base=0.1)
+    bnodes = [x for x in g.nodes if 0 in x or 39 in x]  # grid_chain_sec11.py:225-233
+    part.updaters["boundary"] = lambda p: bnodes
+    pb = gc.within_percent_of_ideal_population(part, 0.10)
+    fn = gc.annealing_cut_accept_backwards if accept == "annealing" else gc.uniform_accept
+    chain = gc.MarkovChain(gc.slow_reversible_propose_bi, gc.Validator(
+        [gc.single_flip_contiguous, pb]), accept=fn, initial_state=part, total_steps=801, seed=2)
+    res = chain.run_batched(3, chain_id0=7)
+    lo, hi = population_bounds(g.n, 2, 0.10)
+    flags = boundary_flags(g)
+    assert flags.sum() == len(bnodes)
+    thr = annealing_table(0.1, 5, 4) if accept == "annealing" else metropolis_table(1.0, 4)
+    for i in range(3):
+        olab, ost, _, _ = O.run_chain(g, sec11_seed(g, 1), 2, 0, lo, hi, thr, 2, 7 + i, 800,
+                                      accept_rule=1 if accept == "annealing" else 2, flags=flags)
+        assert np.array_equal(res.labels[i], olab)
+        assert res.stats["accepts"][i] == ost["accepts"][0]

@@ -131,3 +131,13 @@ def test_delaunay_c4_graph_and_tree_seed():
     lab = recursive_tree_part(g, list(range(k)), g.total_pop / k, 0.05, seed=0)
     lo, hi = population_bounds(g.total_pop, k, 0.05)
     assert O.plan_valid(g, lab, k, lo, hi)  # the debt rule keeps the remainder in bounds too
+
+
+def test_write_wait_txt(tmp_path):
+    from flipcomplexityempirical_amd.chain import write_wait_txt
+    st = np.zeros(1, O.STATS_DTYPE)
+    st["sum_invb"], st["yields"] = [250.5], [100000]
+    w = expected_wait_sum(st, 1596, 2)[0]
+    p = tmp_path / "2B10P5wait.txt"  # grid_chain_sec11.py:410 naming
+    write_wait_txt(str(p), w)
+    assert p.read_text() == str(int(round(w))) and "\n" not in p.read_text()
