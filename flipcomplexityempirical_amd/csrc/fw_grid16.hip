@@ -77,6 +77,14 @@ __device__ __forceinline__ uint32_t row_last(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x15F, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint32_t row_sum(uint32_t x) { return row_last(row_scan(x)); }
+// lane 0 of each row broadcast to the row (row_newbcast:0)
+__device__ __forceinline__ uint32_t row_first(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150, 0xF, 0xF, false);
+}
+// lane q takes lane q+1 of its row (row_shl:1; lane 15 gets 0)
+__device__ __forceinline__ uint32_t row_shl1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);
+}
 // value held by row-lane L (row-uniform L in 0..15; anything else gives 0)
 __device__ __forceinline__ uint32_t row_pick(uint32_t x, int L, int q) {
   return row_sum(q == L ? x : 0u);
@@ -467,8 +475,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     observe(has && !stuck && yields0 == 0 && attempts == 0);
 
     // Philox batches: lane q of a row holds the draw of its chain's attempt (base + q).
-    // Active rows consume one attempt per loop iteration in lockstep, so every row reads
-    // lane `bpos` of its own row; a row that stops stays stopped for this launch.
+    // Active rows consume one attempt per loop iteration in lockstep: each iteration
+    // broadcasts lane 0 of the row (row_newbcast:0) and shifts the batch down one lane
+    // (row_shl:1), all DPP; a row that stops stays stopped for this launch.
     U4 pb = {0u, 0u, 0u, 0u};
     int bpos = ROW;
 
@@ -486,11 +495,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
                     in_vgpr(key0), in_vgpr(key1));
         bpos = 0;
       }
-      const int srcl = (row * ROW + bpos) * 4;  // ds_bpermute byte address of the source lane
-      const U4 x = {(uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x0),
-                    (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x1),
-                    (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x2),
-                    (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)pb.x3)};
+      // lane 0 of the row holds this attempt's draw; shift the batch for the next one
+      const U4 x = {row_first(pb.x0), row_first(pb.x1), row_first(pb.x2), row_first(pb.x3)};
+      pb = U4{row_shl1(pb.x0), row_shl1(pb.x1), row_shl1(pb.x2), row_shl1(pb.x3)};
       ++bpos;
       attempts += act ? 1u : 0u;
       const uint32_t r = scale64(x.x0, x.x1, (uint32_t)(npairs > 0 ? npairs : 1));

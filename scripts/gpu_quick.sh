@@ -1,0 +1,13 @@
+#!/bin/bash
+# Quick GPU iteration: every gpu test (quiet), then a short default bench line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
+timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 10 ${BENCH_ARGS:-} \
+    > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || { tail -5 gpurun_out/bench_quick.err; exit 1; }
+cut -c1-220 gpurun_out/bench_quick.json
+exit $rc
