@@ -84,12 +84,14 @@ struct fw_graph {
   int32_t* d_eid = nullptr;  // [nnz] canonical edge id per CSR entry
   int32_t* d_eu = nullptr;   // [E] canonical edge endpoints (u < w)
   int32_t* d_ew = nullptr;
+  uint64_t* d_nbadj = nullptr;  // [nnz] (general graphs): adjacency among v's neighbours
   int64_t popof(int x) const { return pop.empty() ? 1 : pop[x]; }
   FwGraphDev dev() const {
     FwGraphDev g;
     g.rowptr = d_rowptr;
     g.col = d_col;
     g.eid = d_eid;
+    g.nbadj = d_nbadj;
     g.pop = d_pop;
     g.n = n;
     g.nedges = nnz / 2;
@@ -276,12 +278,25 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
       }
     }
   const size_t ne = std::max<size_t>(eu.size(), 1);
+  // general graphs: for entry (v, i), the positions j of v's neighbours adjacent to the
+  // i-th (the kernel's local contiguity test; degrees <= 63 were checked above)
+  std::vector<uint64_t> nbadj;
+  if (!g->gw && nnz > 0 && g->maxdeg <= 63) {
+    nbadj.assign(nnz, 0);
+    for (int v = 0; v < n; ++v)
+      for (int i = rowptr[v]; i < rowptr[v + 1]; ++i)
+        for (int j = rowptr[v]; j < rowptr[v + 1]; ++j)
+          if (j != i && std::binary_search(col + rowptr[col[i]], col + rowptr[col[i] + 1], col[j]))
+            nbadj[i] |= 1ull << (j - rowptr[v]);
+  }
   hipError_t e1 = hipMalloc(&g->d_rowptr, sizeof(int32_t) * (n + 1));
   hipError_t e2 = hipMalloc(&g->d_col, sizeof(int32_t) * std::max(nnz, 1));
   hipError_t e3 = g->pop.empty() ? hipSuccess : hipMalloc(&g->d_pop, sizeof(int64_t) * n);
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_eid, sizeof(int32_t) * eid.size());
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_eu, sizeof(int32_t) * ne);
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_ew, sizeof(int32_t) * ne);
+  if (e3 == hipSuccess && !nbadj.empty())
+    e3 = hipMalloc(&g->d_nbadj, sizeof(uint64_t) * nbadj.size());
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
     fw_graph_destroy(g);
     return fail(FW_EHIP, "hipMalloc failed for graph");
@@ -294,6 +309,9 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
           hipSuccess;
   up &= hipMemcpy(g->d_eid, eid.data(), sizeof(int32_t) * eid.size(), hipMemcpyHostToDevice) ==
         hipSuccess;
+  if (!nbadj.empty())
+    up &= hipMemcpy(g->d_nbadj, nbadj.data(), sizeof(uint64_t) * nbadj.size(),
+                    hipMemcpyHostToDevice) == hipSuccess;
   if (!eu.empty()) {
     up &= hipMemcpy(g->d_eu, eu.data(), sizeof(int32_t) * eu.size(), hipMemcpyHostToDevice) ==
           hipSuccess;
@@ -317,6 +335,7 @@ void fw_graph_destroy(fw_graph* g) {
   if (g->d_eid) (void)hipFree(g->d_eid);
   if (g->d_eu) (void)hipFree(g->d_eu);
   if (g->d_ew) (void)hipFree(g->d_ew);
+  if (g->d_nbadj) (void)hipFree(g->d_nbadj);
   delete g;
 }
 

@@ -593,6 +593,36 @@ struct Ctx {
     if (m == 0) return false;
     if (m == 1) return true;
     uint64_t cls = lane < m ? (1ull << lane) : 0ull;
+    // source index (rank in am) of the source held by lane ln
+    auto sx = [&](int ln) { return __popcll(am & ((1ull << ln) - 1ull)); };
+    auto merge = [&](int s1, int s2) {
+      const uint64_t nm = rdl64(cls, s1) | rdl64(cls, s2);
+      if (lane < m && ((nm >> lane) & 1ull)) cls = nm;
+    };
+    if constexpr (!GRID) {
+      // sources joined by a direct edge form one local component (the same links as the
+      // oracle's contiguous_after): one component is connected; otherwise pre-merge
+      const int e0 = g.rowptr[v];
+      const uint64_t adjl = ((am >> lane) & 1ull) ? (g.nbadj[e0 + lane - 1] << 1) & am : 0ull;
+      uint64_t comp = am & (~am + 1ull);  // the lowest source
+      for (;;) {
+        const uint64_t nxt = comp | wave_or64(((comp >> lane) & 1ull) ? adjl : 0ull);
+        if (nxt == comp) break;
+        comp = nxt;
+      }
+      if (comp == am) return true;
+      uint64_t todo = am;
+      while (todo) {
+        const int Ls = __ffsll((unsigned long long)todo) - 1;
+        todo &= todo - 1;
+        uint64_t nb = rdl64(adjl, Ls) & ~((2ull << Ls) - 1ull);  // each pair once
+        while (nb) {
+          const int Lt = __ffsll((unsigned long long)nb) - 1;
+          nb &= nb - 1;
+          merge(sx(Ls), sx(Lt));
+        }
+      }
+    }
     if constexpr (GRID) {
       const uint64_t rb = ballot(lane >= 1 && lane <= 8 && h.lx == a) >> 1;
       const int pN = rb & 1, pW = (rb >> 1) & 1, pE = (rb >> 2) & 1, pS = (rb >> 3) & 1;
@@ -611,12 +641,7 @@ struct Ctx {
         const int wv = window_verdict(A);
         if (wv >= 0) return wv == 1;
       }
-      // pre-merge the ring links; source index of lane l = rank of l among am's bits
-      auto sx = [&](int ln) { return __popcll(am & ((1ull << ln) - 1ull)); };
-      auto merge = [&](int s1, int s2) {
-        const uint64_t nm = rdl64(cls, s1) | rdl64(cls, s2);
-        if (lane < m && ((nm >> lane) & 1ull)) cls = nm;
-      };
+      // pre-merge the ring links
       if (lNE) merge(sx(1), sx(3));
       if (lES) merge(sx(3), sx(4));
       if (lSW) merge(sx(4), sx(2));

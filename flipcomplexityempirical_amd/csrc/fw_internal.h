@@ -16,6 +16,7 @@ struct FwGraphDev {
   const int32_t* rowptr;  // [n+1]
   const int32_t* col;     // [nnz]
   const int32_t* eid;     // [nnz] canonical edge id of each CSR entry
+  const uint64_t* nbadj;  // [nnz] entry (v, i): bit j set iff neighbours i and j of v are adjacent
   const int64_t* pop;     // [n] or nullptr (unit populations)
   int32_t n, nedges, maxdeg;
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)

@@ -346,7 +346,29 @@ static int contiguous_after(chain_t* c, int32_t v, int16_t a, int count) {
     const int wv = orc_window_verdict(window_mask(c, v, a));
     if (wv >= 0) return wv;
   } else {
+    /* general graphs: sources joined by a direct edge are one local component; a single
+     * component is connected without a search (the kernels test the same links with a
+     * per-CSR-entry neighbour bitmask), otherwise the links pre-merge the search */
     for (int32_t i = 0; i < m; ++i) uf[i] = i;
+    int32_t comps = m;
+    for (int32_t i = 0; i < m; ++i)
+      for (int32_t j = i + 1; j < m; ++j) {
+        const int32_t* b = g->col + g->rowptr[src[i]];
+        const int32_t* e = g->col + g->rowptr[src[i] + 1];
+        int32_t lo = 0, hi = (int32_t)(e - b);
+        while (lo < hi) { /* src[j] in the (ascending) row of src[i]? */
+          const int32_t mid = (lo + hi) / 2;
+          if (b[mid] < src[j]) lo = mid + 1; else hi = mid;
+        }
+        if (lo < (int32_t)(e - b) && b[lo] == src[j]) {
+          const int32_t ri = uf_find(uf, i), rj = uf_find(uf, j);
+          if (ri != rj) {
+            uf[ri] = rj;
+            --comps;
+          }
+        }
+      }
+    if (comps == 1) return 1;
   }
   if (count) c->st.bfs_runs++;
   int32_t nl = 0;

@@ -167,6 +167,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["waits"]:
         wait_fixtures()
         sys.exit(0)
+    if sys.argv[1:] == ["chains"]:
+        chain_fixtures()
+        sys.exit(0)
     kansas_fixtures()
     wait_fixtures()
     flip_fixtures()
