@@ -156,6 +156,10 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N>1 (nccl = RCCL over xGMI; gloo for rehearsals)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="put every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)")
     ap.add_argument("--maps", action="store_true",
                     help="also keep the spatial observables (cut_times, part_sum, ...) per chain")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
@@ -166,12 +170,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = 0 if args.same_device else local_rank
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.backend)
+    tdev = "cuda" if args.backend == "nccl" else "cpu"
     from flipcomplexityempirical_amd.chain import (PROPOSALS, Chains, DeviceGraph,
                                                    population_bounds)
     from flipcomplexityempirical_amd.distributed import merge_histograms
@@ -190,17 +196,17 @@ def main():
         base = args.base if args.base is not None else base
         base_desc = f"base {base:.9g}"
     bounds = population_bounds(g.total_pop, k, percent)
-    dg = DeviceGraph(g, device=local_rank)
+    dg = DeviceGraph(g, device=device)
     ch = Chains(dg, chains, k, init, proposal=proposal, pop_bounds=bounds, base=base,
                 seed=args.seed, chain_id0=cid0)
     if args.maps:
         ch.enable_maps([-1, 1] if k == 2 else None)
 
     def barrier():
-        torch.cuda.synchronize(local_rank)
+        torch.cuda.synchronize(device)
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize(local_rank)
+        torch.cuda.synchronize(device)
 
     for _ in range(args.warmup):
         ch.run(args.inner)
@@ -219,7 +225,7 @@ def main():
     d = {kk: st1[kk] - st0[kk] for kk in st1}
     steps_local = d["steps"]
     if dist is not None:
-        t = torch.tensor([dt, float(steps_local)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt, float(steps_local)], dtype=torch.float64, device=tdev)
         dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
         dt, steps_all = float(t[0]), float(t[1])
