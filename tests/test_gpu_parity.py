@@ -212,3 +212,30 @@ def test_accept_rules_bit_exact(gpu_lib, name, rule, path, monkeypatch):
         assert np.array_equal(labs[i], lab), (name, i)
         for f in ("attempts", "steps", "accepts", "sum_cut", "bnodes", "bfs_nodes"):
             assert st[f][i] == ost[f][0], (name, i, f)
+
+
+@pytest.mark.parametrize("n,k,bw", [(132, 8, 4), (200, 8, 4)])
+def test_large_grid_ladder_bit_exact(gpu_lib, n, k, bw, monkeypatch):
+    """C5 shape: grids past the four-chains-per-wave kernel's 16,384-node limit (one chain
+    per wave, implicit grid neighbours, 16 group sums per lane) with per-chain Metropolis
+    bases from the C5 ladder (thr_per_chain)."""
+    from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    g = grid_graph(n, n)
+    init = block_seed(n, n, 2, bw)
+    bounds = population_bounds(g.total_pop, k, 0.05)
+    bases = np.geomspace(0.1, 10.0, 5)
+    dg = DeviceGraph(g)
+    ch = Chains(dg, len(bases), k, init, proposal="pairs", pop_bounds=bounds, base=bases, seed=8,
+                chain_id0=1000)
+    for s in (500, 300):
+        ch.run(s)
+    labs, st = ch.labels(), ch.stats()
+    for i, b in enumerate(bases):
+        lab, ost = init.copy(), O.new_stats(1)
+        for s in (500, 300):
+            lab, ost, _, _ = O.run_chain(g, lab, k, 1, *bounds, metropolis_table(b, 4), 8, 1000 + i,
+                                         s, stats=ost)
+        assert np.array_equal(labs[i], lab), i
+        assert_stats_equal(st[i:i + 1], ost)
