@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
@@ -100,6 +101,7 @@ struct fw_graph {
     g.gh = gh;
     // exact x / gw for x < 2^21 (the grid path is only taken for n < 2^21)
     g.gmagic = gw ? (((uint64_t)1 << 42) + (uint64_t)gw - 1) / (uint64_t)gw : 0;
+    g.gm32 = gw ? (uint32_t)((((uint64_t)1 << 32) + (uint64_t)gw - 1) / (uint64_t)gw) : 0;
     return g;
   }
 };
@@ -115,6 +117,7 @@ struct fw_chains {
   fw_chain_stats* d_stats = nullptr;
   int64_t* d_pops = nullptr;
   double* d_thr = nullptr;
+  uint64_t* d_thr53 = nullptr;
   unsigned long long* d_hist_cut = nullptr;
   unsigned long long* d_hist_b = nullptr;
   uint32_t* d_spill = nullptr;
@@ -353,7 +356,7 @@ void fw_chains_destroy(fw_chains* c) {
   if (!c) return;
   (void)hipSetDevice(c->g->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr,  c->d_hist_cut, c->d_hist_b,
+  void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_thr53, c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
                   c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt};
   for (void* b : bufs)
@@ -383,7 +386,9 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   // row-major grids: the four-chains-per-wave kernel, 2-bit labels when k <= 4
   // (FLIPWALK_NO_GRID16=1 forces the one-chain-per-wave kernel, for A/B parity tests)
   const char* no16 = getenv("FLIPWALK_NO_GRID16");
-  const bool use16 = fw_grid16_candidate(g->gw, D, G, k) && !(no16 && no16[0] == '1');
+  int64_t total_pop = 0;
+  for (int x = 0; x < n; ++x) total_pop += g->popof(x);
+  const bool use16 = fw_grid16_candidate(g->gw, D, G, k, total_pop) && !(no16 && no16[0] == '1');
   const int lb = use16 ? (k <= 4 ? 2 : 4) : pick_lb(k, g->maxdeg);
   if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 
@@ -464,10 +469,18 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     return fail(FW_EHIP, "occupancy query failed (LDS %d B)", use16 ? p.lds16 : p.lds_bytes);
   }
   const size_t nthr = (size_t)(thr_per_chain ? n_chains : 1) * (2 * D + 1);
+  // integer form of the Metropolis bound: CPython's u = M * 2^-53 with integer M < 2^53,
+  // so u < thr <=> M < thr * 2^53 (exact scaling) <=> M < ceil(thr * 2^53)
+  std::vector<uint64_t> thr53(nthr);
+  for (size_t i = 0; i < nthr; ++i) {
+    const double t = thr[i] * 9007199254740992.0;
+    thr53[i] = !(t > 0.0) ? 0ull : (t >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)std::ceil(t));
+  }
   bool ok = hipMalloc(&c->d_labels, packed.size()) == hipSuccess &&
             hipMalloc(&c->d_stats, sizeof(fw_chain_stats) * n_chains) == hipSuccess &&
             hipMalloc(&c->d_pops, sizeof(int64_t) * pops.size()) == hipSuccess &&
             hipMalloc(&c->d_thr, sizeof(double) * nthr) == hipSuccess &&
+            hipMalloc(&c->d_thr53, sizeof(uint64_t) * nthr) == hipSuccess &&
             hipMalloc(&c->d_hist_cut, sizeof(unsigned long long) * (g->nnz / 2 + 1 + FW_HIST_PAD)) ==
                 hipSuccess &&
             hipMalloc(&c->d_hist_b, sizeof(unsigned long long) * (n + 1 + FW_HIST_PAD)) ==
@@ -485,6 +498,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
        hipMemcpy(c->d_pops, pops.data(), sizeof(int64_t) * pops.size(), hipMemcpyHostToDevice) ==
            hipSuccess &&
        hipMemcpy(c->d_thr, thr, sizeof(double) * nthr, hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemcpy(c->d_thr53, thr53.data(), sizeof(uint64_t) * nthr, hipMemcpyHostToDevice) ==
+           hipSuccess &&
        hipMemset(c->d_stats, 0, sizeof(fw_chain_stats) * n_chains) == hipSuccess &&
        hipMemset(c->d_hist_cut, 0, sizeof(unsigned long long) * (g->nnz / 2 + 1 + FW_HIST_PAD)) ==
            hipSuccess &&
@@ -497,6 +512,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.stats = c->d_stats;
   p.pops = c->d_pops;
   p.thr = c->d_thr;
+  p.thr53 = c->d_thr53;
   p.hist_cut = c->d_hist_cut;
   p.hist_b = c->d_hist_b;
   p.spill = c->d_spill;

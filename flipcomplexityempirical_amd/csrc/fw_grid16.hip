@@ -110,7 +110,7 @@ __device__ __forceinline__ uint32_t lab_window(const LDS uint8_t* lab, int x) {
 // four nodes has that neighbour; per-node row/column checks mask the rest.
 template <int LB, int MODE>
 __device__ __forceinline__ void weights4(const LDS uint8_t* lab, int x0, int W, int H, int n,
-                                         uint64_t gmagic, uint32_t& w4, uint32_t& cd4) {
+                                         uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
   constexpr uint32_t M = (1u << LB) - 1u;
   w4 = 0;
   cd4 = 0;
@@ -118,7 +118,7 @@ __device__ __forceinline__ void weights4(const LDS uint8_t* lab, int x0, int W, 
   const uint32_t own = lab_window<LB>(lab, x0);
   const uint32_t up = x0 + 3 - W >= 0 ? lab_window<LB>(lab, x0 - W) : 0u;
   const uint32_t dn = x0 + W < n ? lab_window<LB>(lab, x0 + W) : 0u;
-  const int r0 = (int)(((uint64_t)(uint32_t)x0 * gmagic) >> 42);
+  const int r0 = (int)__umulhi((uint32_t)x0, gm32);
   const int c0 = x0 - r0 * W;
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
@@ -174,7 +174,7 @@ __device__ __forceinline__ uint32_t byte_popc(uint32_t f) {  // per-byte popcoun
 
 template <int MODE, bool NEED_CD>
 __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, int W, int H, int n,
-                                              uint64_t gmagic, uint32_t& w4, uint32_t& cd4) {
+                                              uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
   w4 = 0;
   cd4 = 0;
   if (x0 >= n) return;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
   const uint32_t R = __builtin_amdgcn_alignbyte(o_hi, o_lo, 2);  // x+1
   const uint32_t U = onehot4(spread4(up >> 2)), Dn = onehot4(spread4(dn >> 2));
   // which of the four nodes have each neighbour (W >= 4: at most one row wrap, at tw)
-  const int r0 = (int)(((uint64_t)(uint32_t)x0 * gmagic) >> 42);
+  const int r0 = (int)__umulhi((uint32_t)x0, gm32);
   const int c0 = x0 - r0 * W;
   const int tw = W - c0;  // first byte on the next grid row (>= 4: none)
   const uint32_t mN = low_bytes(n - x0);
@@ -211,11 +211,11 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
 // weights (and, when NEED_CD, cut degrees) of nodes x0..x0+3, one per byte
 template <int LB, int MODE, bool NEED_CD>
 __device__ __forceinline__ void weights4x(const LDS uint8_t* lab, int x0, int W, int H, int n,
-                                          uint64_t gmagic, uint32_t& w4, uint32_t& cd4) {
+                                          uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
   if constexpr (LB == 2)
-    weights4_swar<MODE, NEED_CD>(lab, x0, W, H, n, gmagic, w4, cd4);
+    weights4_swar<MODE, NEED_CD>(lab, x0, W, H, n, gm32, w4, cd4);
   else
-    weights4<LB, MODE>(lab, x0, W, H, n, gmagic, w4, cd4);
+    weights4<LB, MODE>(lab, x0, W, H, n, gm32, w4, cd4);
 }
 
 // bytes of w (each < 64) summed
@@ -241,7 +241,7 @@ __device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
 // Wave-cooperative: all 64 lanes call it for one chain; the caller holds the lock.
 template <int LB>
 __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t* list,
-                          GLB uint32_t* spill, int qcap, int W, int H, uint64_t gmagic, int lane,
+                          GLB uint32_t* spill, int qcap, int W, int H, uint32_t gm32, int lane,
                           int v, uint32_t a, int m, int src, uint64_t cls, uint64_t& bfs_nodes,
                           uint64_t& bfs_deg) {
   using P = PK<LB>;
@@ -277,7 +277,7 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
       const bool act = idx < le;
       const int x = act ? (int)list_get(idx) : 0;
       const uint32_t o = act ? S::get(scr, x) - 1u : 0u;
-      const int xr = (int)(((uint64_t)(uint32_t)x * gmagic) >> 42);
+      const int xr = (int)__umulhi((uint32_t)x, gm32);
       const int xc = x - xr * W;
       if (act) my_deg += (uint32_t)((xr > 0) + (xc > 0) + (xc < W - 1) + (xr < H - 1));
       bfs_nodes += (uint64_t)__popcll(ballot(act));
@@ -367,11 +367,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   const uint32_t key0 = (uint32_t)p.seed, key1 = (uint32_t)(p.seed >> 32);
   const int GW = (G + 1) >> 1;  // u16-pair words of group sums
   const bool maps_on = FULL && p.m_acc != nullptr;
+  // population bounds as int32 (the host routes graphs with total population >= 2^31 to
+  // the one-chain-per-wave kernel); clamped so comparisons keep their meaning
+  const int32_t pop_lo = (int32_t)max(p.pop_lo, (int64_t)INT32_MIN);
+  const int32_t pop_hi = (int32_t)min(p.pop_hi, (int64_t)INT32_MAX);
   const int32_t rule = FULL ? p.accept : FW_ACCEPT_CUT;
   int my_dr, my_dc;
   role_off(q <= 8 ? q : 0, my_dr, my_dc);
   auto divmod = [&](int x, int& r, int& c) {
-    r = (int)(((uint64_t)(uint32_t)x * p.g.gmagic) >> 42);
+    r = (int)__umulhi((uint32_t)x, p.g.gm32);
     c = x - r * W;
   };
   STAMP_DECL
@@ -400,8 +404,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(lab);
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
     }
-    int64_t pops = q < k ? p.pops[(size_t)cc * k + q] : 0;
-    const double thr_l = q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
+    int32_t pops = q < k ? (int32_t)p.pops[(size_t)cc * k + q] : 0;  // total pop < 2^31
+    const double thr_l = FULL && q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
+    const uint64_t thr53_l = q < 2 * D + 1 ? p.thr53[(size_t)cc * p.thr_stride + q] : 0ull;
     fw_chain_stats* stp = p.stats + cc;
     uint64_t attempts = stp->attempts;
     const uint64_t yields0 = stp->yields;
@@ -425,7 +430,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           uint32_t w4, cd4;
-          weights4x<LB, MODE, true>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, p.g.gmagic, w4, cd4);
+          weights4x<LB, MODE, true>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, p.g.gm32, w4, cd4);
           const uint32_t ws = bsum4m(w4);
           cut2 += bsum4m(cd4);
           bn += ((cd4 & 0xFFu) != 0) + ((cd4 & 0xFF00u) != 0) + ((cd4 & 0xFF0000u) != 0) +
@@ -517,19 +522,18 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const uint32_t incl = row_scan(s);
       const uint32_t rb1 = rowbits(ballot(incl > r), row);
       const int Lw = __ffs(rb1) - 1;
-      uint32_t rl = r - (incl - s), c1 = 0, before = 0;
-      int tf = PER - 1;
-      bool found = false;
+      // the group holding rank rl among this lane's PER: the count of inclusive prefixes
+      // <= rl, and the last such prefix (prefixes are non-decreasing)
+      const uint32_t rl = r - (incl - s);
+      uint32_t c1 = 0, before = 0, tfu = 0;
 #pragma unroll
       for (int t = 0; t < PER; ++t) {
-        const uint32_t c2 = c1 + gs[t];
-        if (!found && rl < c2) {
-          tf = t;
-          before = c1;
-          found = true;
-        }
-        c1 = c2;
+        c1 += gs[t];
+        const bool le = c1 <= rl;
+        tfu += le ? 1u : 0u;
+        before = le ? c1 : before;
       }
+      const int tf = min((int)tfu, PER - 1);
       // pack (group, remaining rank) into one row broadcast
       const uint32_t pk1 = row_pick(((uint32_t)(q * PER + tf) << 16) | ((rl - before) & 0xFFFFu), Lw, q);
       const int gi = min((int)(pk1 >> 16), G - 1);
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
-      weights4x<LB, MODE, false>(lab, x0, W, H, n, p.g.gmagic, w4, cd4);
+      weights4x<LB, MODE, false>(lab, x0, W, H, n, p.g.gm32, w4, cd4);
       const uint32_t pref = w4 * 0x01010101u;  // byte t: weights of nodes 0..t (<= 16)
       const uint32_t ws = pref >> 24;
       const uint32_t incl2 = row_scan(ws);
@@ -622,9 +626,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const int dcut = m - nbd;
 
       // ---- population bound (lane q holds district q)
-      const int64_t pv = unit_pop ? 1 : p.g.pop[v];
-      const bool bad = ((uint32_t)q == a && pops - pv < p.pop_lo) ||
-                       ((uint32_t)q == d && pops + pv > p.pop_hi);
+      const int32_t pv = unit_pop ? 1 : (int32_t)p.g.pop[v];
+      const bool bad = ((uint32_t)q == a && pops - pv < pop_lo) ||
+                       ((uint32_t)q == d && pops + pv > pop_hi);
       const bool pop_ok = rowbits(ballot(bad), row) == 0u;
 
       STAMP(3);  // gather, target, Δcut, population
@@ -696,7 +700,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (lk & 8) merge(sx(1), sx(0));  // W-N
         uint64_t bn = 0, bd = 0;
         const bool ok = grid_race<LB>(sm + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
-                                      p.qcap16, W, H, p.g.gmagic, lane, vv, aa, mr, srcn, cls, bn,
+                                      p.qcap16, W, H, p.g.gm32, lane, vv, aa, mr, srcn, cls, bn,
                                       bd);
         if (row == rr) {
           contig = ok;
@@ -750,10 +754,13 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       } else {
         // cut_accept (grid_chain_sec11.py:171-179), or with the |B'|/|B| factor of
         // annealing_cut_accept_backwards (:81-110)
-        const double bound = rule == FW_ACCEPT_BRATIO
-                                 ? thr_l * ((double)(bnodes + plus - minus) / (double)bnodes)
-                                 : thr_l;
-        const bool acc_l = u53(x.x2, x.x3) < bound;
+        bool acc_l;
+        if (rule == FW_ACCEPT_BRATIO) {
+          const double bound = thr_l * ((double)(bnodes + plus - minus) / (double)bnodes);
+          acc_l = u53(x.x2, x.x3) < bound;
+        } else {  // integer form of u53(x2, x3) < thr_l (exact)
+          acc_l = (((uint64_t)(x.x2 >> 5) << 26) | (uint64_t)(x.x3 >> 6)) < thr53_l;
+        }
         accepted = valid && ((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u);
       }
       if (valid && p.trace && q == 0)
@@ -811,7 +818,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
-      if (q < k) p.pops[(size_t)c * k + q] = pops;
+      if (q < k) p.pops[(size_t)c * k + q] = (int64_t)pops;
       if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
       if (q == 0 && maps_on) pend_store(p, c, pend);
       if (q == 0) {
@@ -873,9 +880,10 @@ extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-bool fw_grid16_candidate(int gw, int maxdeg, int G, int k) {
-  // gw >= 4: four consecutive nodes span at most one row wrap (weights4_swar masks)
-  return gw >= 4 && maxdeg == 4 && G <= 16 * 16 && k <= 15;
+bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop) {
+  // gw >= 4: four consecutive nodes span at most one row wrap (weights4_swar masks);
+  // populations are held as int32
+  return gw >= 4 && maxdeg == 4 && G <= 16 * 16 && k <= 15 && total_pop < (1ll << 31) - 1;
 }
 
 void* fw_grid16_fn(const FwRunParams& p) {

@@ -21,6 +21,7 @@ struct FwGraphDev {
   int32_t n, nedges, maxdeg;
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)
   uint64_t gmagic;        // ceil(2^42 / gw): x / gw == (x * gmagic) >> 42 for x < 2^21
+  uint32_t gm32;          // ceil(2^32 / gw): x / gw == mulhi(x, gm32) for x * gw < 2^32
 };
 
 struct FwRunParams {
@@ -30,6 +31,8 @@ struct FwRunParams {
   fw_chain_stats* stats;       // [n_chains]
   int64_t* pops;               // [n_chains][k]
   const double* thr;           // [n_chains or 1][2*maxdeg+1]
+  const uint64_t* thr53;       // same shape: ceil(thr * 2^53) clamped to 2^53 (u < thr <=>
+                               // u * 2^53 < thr53 for CPython's 53-bit u)
   int32_t thr_stride;          // 0 (shared table) or 2*maxdeg+1
   unsigned long long* hist_cut;  // [nedges+1+FW_HIST_PAD]
   unsigned long long* hist_b;    // [n+1+FW_HIST_PAD]
@@ -115,7 +118,7 @@ int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);
 // fw_grid16.hip
-bool fw_grid16_candidate(int gw, int maxdeg, int G, int k);
+bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop);
 void* fw_grid16_fn(const FwRunParams& p);
 int fw_grid16_plan(FwRunParams& p, int device, int* grid);
 int fw_grid16_launch(const FwRunParams& p, int grid, void* stream);
