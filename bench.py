@@ -237,11 +237,23 @@ def main():
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
+    issue = None
     default_c3 = (args.config, g.n, k, chains, args.inner, proposal) == (
         "c3", 10000, 4, 65536, 1000, "pairs")
     if default_c3 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)
+        traffic = tj.get("hbm_bytes_per_launch")
+        if tj.get("valu_insts_per_launch"):
+            # what binds this kernel: VALU issue.  Peak: every SIMD takes one wave64 VALU
+            # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md) -> 256 CUs x 4 SIMDs
+            # x 2.4 GHz / 2; achieved: the PMC pass's VALU wave-instructions per launch
+            # over this run's mean launch time.
+            peak = 256 * 4 * 2.4e9 / 2
+            ach = tj["valu_insts_per_launch"] / (kernel_ms * 1e-3)
+            issue = {"bound": "valu-issue", "achieved": ach, "peak": peak,
+                     "unit": "wave-instr/s", "frac": ach / peak,
+                     "source": tj.get("source")}
 
     if rank == 0:
         out = {
@@ -273,6 +285,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
             },
+            "issue_roofline": issue,
             "kernel_ms": kernel_ms,
             "proposals_per_s": d["attempts"] * world / dt,
             "accepts_per_s": d["accepts"] * world / dt,

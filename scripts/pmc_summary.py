@@ -29,12 +29,21 @@ for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg.items()):
     print(f"{k:28s} {sum(v)/len(v):16.4g}  (n={len(v)})")
+def _mean(name):
+    v = agg.get(name)
+    return sum(v) / len(v) if v else None
+
+
 if len(sys.argv) > 2 and "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
     fetch = sum(agg["FETCH_SIZE"]) / len(agg["FETCH_SIZE"]) * 1024.0
     write = sum(agg["WRITE_SIZE"]) / len(agg["WRITE_SIZE"]) * 1024.0
     out = {"hbm_bytes_per_launch": 2.0 * fetch + write, "fetch_bytes_raw": fetch,
            "fetch_bytes_corrected": 2.0 * fetch, "write_bytes": write,
            "source": os.path.basename(os.path.normpath(d)), "kernel_trace": kern,
+           # instruction issue per launch (the kernel's binding resource), for bench.py's
+           # issue roofline: wave-instructions, SQ_INSTS_* summed over the chip
+           "valu_insts_per_launch": _mean("SQ_INSTS_VALU"), "salu_insts_per_launch": _mean("SQ_INSTS_SALU"),
+           "lds_insts_per_launch": _mean("SQ_INSTS_LDS"), "waves": _mean("SQ_WAVES"),
            "note": "FETCH_SIZE x2 (gfx950 coalesced-read correction) + WRITE_SIZE, KB->B"}
     with open(sys.argv[2], "w") as f:
         json.dump(out, f, indent=1)
