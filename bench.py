@@ -253,7 +253,9 @@ def main():
             ach = tj["valu_insts_per_launch"] / (kernel_ms * 1e-3)
             issue = {"bound": "valu-issue", "achieved": ach, "peak": peak,
                      "unit": "wave-instr/s", "frac": ach / peak,
-                     "source": tj.get("source")}
+                     "source": tj.get("source"),
+                     # rocprofv3 --kernel-trace --stats mean of the same kernel, same command
+                     "rocprof_kernel_ms": (tj.get("kernel_trace") or {}).get("avg_ms")}
 
     if rank == 0:
         out = {

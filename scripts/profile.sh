@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r01}
 shift
-BENCH_ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --inner 1000 --no-cpu-baseline"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --inner 1000 --no-cpu-baseline"}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
