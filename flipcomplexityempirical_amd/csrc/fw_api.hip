@@ -86,6 +86,7 @@ struct fw_graph {
   int32_t* d_eu = nullptr;   // [E] canonical edge endpoints (u < w)
   int32_t* d_ew = nullptr;
   uint64_t* d_nbadj = nullptr;  // [nnz] (general graphs): adjacency among v's neighbours
+  int32_t* d_ell = nullptr;     // [n][16] (general graphs, max degree <= 16): padded rows
   int64_t popof(int x) const { return pop.empty() ? 1 : pop[x]; }
   FwGraphDev dev() const {
     FwGraphDev g;
@@ -93,6 +94,7 @@ struct fw_graph {
     g.col = d_col;
     g.eid = d_eid;
     g.nbadj = d_nbadj;
+    g.ell = d_ell;
     g.pop = d_pop;
     g.n = n;
     g.nedges = nnz / 2;
@@ -300,6 +302,13 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_ew, sizeof(int32_t) * ne);
   if (e3 == hipSuccess && !nbadj.empty())
     e3 = hipMalloc(&g->d_nbadj, sizeof(uint64_t) * nbadj.size());
+  std::vector<int32_t> ell;
+  if (!g->gw && g->maxdeg <= 16) {
+    ell.assign((size_t)n * 16, -1);
+    for (int x = 0; x < n; ++x)
+      for (int t = rowptr[x]; t < rowptr[x + 1]; ++t) ell[(size_t)x * 16 + (t - rowptr[x])] = col[t];
+    if (e3 == hipSuccess) e3 = hipMalloc(&g->d_ell, sizeof(int32_t) * ell.size());
+  }
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
     fw_graph_destroy(g);
     return fail(FW_EHIP, "hipMalloc failed for graph");
@@ -315,6 +324,9 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   if (!nbadj.empty())
     up &= hipMemcpy(g->d_nbadj, nbadj.data(), sizeof(uint64_t) * nbadj.size(),
                     hipMemcpyHostToDevice) == hipSuccess;
+  if (!ell.empty())
+    up &= hipMemcpy(g->d_ell, ell.data(), sizeof(int32_t) * ell.size(), hipMemcpyHostToDevice) ==
+          hipSuccess;
   if (!eu.empty()) {
     up &= hipMemcpy(g->d_eu, eu.data(), sizeof(int32_t) * eu.size(), hipMemcpyHostToDevice) ==
           hipSuccess;
@@ -339,6 +351,7 @@ void fw_graph_destroy(fw_graph* g) {
   if (g->d_eu) (void)hipFree(g->d_eu);
   if (g->d_ew) (void)hipFree(g->d_ew);
   if (g->d_nbadj) (void)hipFree(g->d_nbadj);
+  if (g->d_ell) (void)hipFree(g->d_ell);
   delete g;
 }
 

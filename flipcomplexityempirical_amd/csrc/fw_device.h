@@ -263,7 +263,11 @@ struct Hood {
   int deg;        // degree of x
 };
 
-template <int LB, bool GRID>
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+// E16: a general graph of max degree <= 16 whose adjacency rows are read from the padded
+// 16-wide table (four 16-byte loads in flight together) instead of walking CSR entries.
+template <int LB, bool GRID, bool E16 = false>
 struct Ctx {
   using P = PK<LB>;
   FwGraphDev g;
@@ -310,6 +314,18 @@ struct Ctx {
       return e < g.rowptr[x + 1] ? g.col[e] : -1;
     }
   }
+  // x's neighbours (CSR order, -1 padding) from the padded table
+  __device__ __forceinline__ void row16(int x, int (&r)[16]) const {
+    const i32x4* p4 = reinterpret_cast<const i32x4*>(g.ell + (size_t)x * 16);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const i32x4 q = p4[t];
+      r[4 * t] = q.x;
+      r[4 * t + 1] = q.y;
+      r[4 * t + 2] = q.z;
+      r[4 * t + 3] = q.w;
+    }
+  }
   __device__ __forceinline__ int degree(int x, int xr, int xc) const {
     if constexpr (GRID) {
       return (xr > 0) + (xc > 0) + (xc < g.gw - 1) + (xr < g.gh - 1);
@@ -324,9 +340,23 @@ struct Ctx {
     int xr = 0, xc = 0;
     if constexpr (GRID) divmod(x, xr, xc);
     const uint32_t lx = L(x);
-    const int dx = GRID ? 4 : g.rowptr[x + 1] - g.rowptr[x];
     uint64_t bits = 0;
     cd = 0;
+    if constexpr (E16) {
+      int r[16];
+      row16(x, r);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j >= g.maxdeg) break;  // uniform
+        const int y = r[j];
+        const uint32_t ly = L(y >= 0 ? y : x);
+        bits |= y >= 0 ? 1ull << ly : 0ull;
+        cd += (y >= 0 && ly != lx) ? 1u : 0u;
+      }
+      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : (uint32_t)__popcll(bits & ~(1ull << lx));
+      return;
+    }
+    const int dx = GRID ? 4 : g.rowptr[x + 1] - g.rowptr[x];
     for (int j = 0; j < dx; ++j) {
       const int y = nbr(x, j, xr, xc);
       if (y < 0) continue;
@@ -408,6 +438,21 @@ struct Ctx {
       h.lx = L(h.x);
       const int f0 = g.rowptr[h.x], f1 = g.rowptr[h.x + 1];
       h.deg = f1 - f0;
+      if constexpr (E16) {
+        int r[16];
+        row16(h.x, r);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (j >= g.maxdeg) break;  // uniform
+          const int y = r[j];
+          const bool ok = y >= 0 && y != v;
+          const uint32_t ly = L(ok ? y : h.x);
+          h.has_v = h.has_v || y == v;
+          h.bits |= ok ? 1ull << ly : 0ull;
+          h.cnt += (ok && ly != h.lx) ? 1u : 0u;
+        }
+        return h;
+      }
       for (int e = f0; e < f1; ++e) {
         const int y = g.col[e];
         if (y == v) {
@@ -519,8 +564,17 @@ struct Ctx {
           for (int d = 32; d >= 1; d >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, d, WAVE));
           jmax = (int)rfl(dm);
         }
-        for (int j = 0; j < jmax; ++j) {
-          const int y = (act && j < dmax) ? nbr(x, j, xr, xc) : -1;
+        int r16[16];
+        if constexpr (E16) {
+          if (act) row16(x, r16);
+        }
+        for (int j = 0; j < (E16 ? 16 : 64); ++j) {  // r16[j]: uniform j (v_movrels)
+          if (j >= jmax) break;  // uniform
+          int y;
+          if constexpr (E16)
+            y = (act && j < dmax) ? r16[j] : -1;
+          else
+            y = (act && j < dmax) ? nbr(x, j, xr, xc) : -1;
           bool push = false, req = false;
           uint32_t other = 0;
           if (y >= 0) {

@@ -17,6 +17,7 @@ struct FwGraphDev {
   const int32_t* col;     // [nnz]
   const int32_t* eid;     // [nnz] canonical edge id of each CSR entry
   const uint64_t* nbadj;  // [nnz] entry (v, i): bit j set iff neighbours i and j of v are adjacent
+  const int32_t* ell;     // [n][16] neighbours padded with -1 (general graphs, max degree <= 16)
   const int64_t* pop;     // [n] or nullptr (unit populations)
   int32_t n, nedges, maxdeg;
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)

@@ -29,10 +29,10 @@
 namespace {
 
 // ---------------------------------------------------------------- the chain kernel
-template <int LB, bool GRID, int MODE, int PER>
+template <int LB, bool GRID, int MODE, int PER, bool E16>
 __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
   extern __shared__ __align__(16) uint8_t smem[];
-  Ctx<LB, GRID> C;
+  Ctx<LB, GRID, E16> C;
   C.g = p.g;
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
   C.lab = sm;
@@ -411,22 +411,25 @@ __global__ void fw_map_read_kernel(FwMapRead m) {
   }
 }
 
-template <int LB, bool GRID, int MODE>
+template <int LB, bool GRID, int MODE, bool E16>
 void* pick_per(int G) {
-  if (G <= 64 * 2) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2>);
-  if (G <= 64 * 4) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4>);
-  if (G <= 64 * 8) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8>);
-  return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16>);
+  if (G <= 64 * 2) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16>);
+  if (G <= 64 * 4) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16>);
+  if (G <= 64 * 8) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16>);
+  return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16>);
 }
 
-void* pick_run(int lb, bool grid, int mode, int G) {
+// grids: implicit neighbours; general graphs: the padded 16-wide table when it exists
+void* pick_run(int lb, bool grid, bool e16, int mode, int G) {
   const bool cut = mode == FW_PROPOSE_CUTEDGE;
   if (lb == 4) {
-    if (grid) return cut ? pick_per<4, true, 2>(G) : pick_per<4, true, 1>(G);
-    return cut ? pick_per<4, false, 2>(G) : pick_per<4, false, 1>(G);
+    if (grid) return cut ? pick_per<4, true, 2, false>(G) : pick_per<4, true, 1, false>(G);
+    if (e16) return cut ? pick_per<4, false, 2, true>(G) : pick_per<4, false, 1, true>(G);
+    return cut ? pick_per<4, false, 2, false>(G) : pick_per<4, false, 1, false>(G);
   }
-  if (grid) return cut ? pick_per<8, true, 2>(G) : pick_per<8, true, 1>(G);
-  return cut ? pick_per<8, false, 2>(G) : pick_per<8, false, 1>(G);
+  if (grid) return cut ? pick_per<8, true, 2, false>(G) : pick_per<8, true, 1, false>(G);
+  if (e16) return cut ? pick_per<8, false, 2, true>(G) : pick_per<8, false, 1, true>(G);
+  return cut ? pick_per<8, false, 2, false>(G) : pick_per<8, false, 1, false>(G);
 }
 
 }  // namespace
@@ -434,7 +437,7 @@ void* pick_run(int lb, bool grid, int mode, int G) {
 // Occupancy-sized persistent grid for the one-chain-per-wave kernel.
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   if (p.G > 64 * 16) return -2;
-  void* fn = pick_run(lb, p.g.gw > 0, p.mode, p.G);
+  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   if (e != hipSuccess) return -1;
   int per_cu = 0;
@@ -450,7 +453,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
 
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   if (p.use16) return fw_grid16_launch(p, grid, stream);
-  void* fn = pick_run(lb, p.g.gw > 0, p.mode, p.G);
+  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G);
   void* args[] = {const_cast<FwRunParams*>(&p)};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes, (hipStream_t)stream);
   return e == hipSuccess ? 0 : -1;
