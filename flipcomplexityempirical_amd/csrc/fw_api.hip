@@ -300,15 +300,21 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_eid, sizeof(int32_t) * eid.size());
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_eu, sizeof(int32_t) * ne);
   if (e3 == hipSuccess) e3 = hipMalloc(&g->d_ew, sizeof(int32_t) * ne);
-  if (e3 == hipSuccess && !nbadj.empty())
-    e3 = hipMalloc(&g->d_nbadj, sizeof(uint64_t) * nbadj.size());
   std::vector<int32_t> ell;
   if (!g->gw && g->maxdeg <= 16) {
+    // padded rows; the neighbour-adjacency masks move to the same [n][16] layout
     ell.assign((size_t)n * 16, -1);
+    std::vector<uint64_t> nb16(nbadj.empty() ? 0 : (size_t)n * 16, 0);
     for (int x = 0; x < n; ++x)
-      for (int t = rowptr[x]; t < rowptr[x + 1]; ++t) ell[(size_t)x * 16 + (t - rowptr[x])] = col[t];
+      for (int t = rowptr[x]; t < rowptr[x + 1]; ++t) {
+        ell[(size_t)x * 16 + (t - rowptr[x])] = col[t];
+        if (!nbadj.empty()) nb16[(size_t)x * 16 + (t - rowptr[x])] = nbadj[t];
+      }
+    nbadj.swap(nb16);
     if (e3 == hipSuccess) e3 = hipMalloc(&g->d_ell, sizeof(int32_t) * ell.size());
   }
+  if (e3 == hipSuccess && !nbadj.empty())
+    e3 = hipMalloc(&g->d_nbadj, sizeof(uint64_t) * nbadj.size());
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
     fw_graph_destroy(g);
     return fail(FW_EHIP, "hipMalloc failed for graph");

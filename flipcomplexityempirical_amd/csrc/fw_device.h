@@ -430,6 +430,29 @@ struct Ctx {
           h.cnt += ly != h.lx;
         }
       }
+    } else if constexpr (E16) {
+      // lanes 1..16 read v's padded row: its neighbours (a prefix) and so its degree
+      const int xn = (lane >= 1 && lane <= 16) ? g.ell[(size_t)v * 16 + lane - 1] : -1;
+      dv = __popcll(ballot(xn >= 0));
+      if (lane > dv) return h;
+      h.x = lane == 0 ? v : xn;
+      h.lx = L(h.x);
+      int r[16];
+      row16(h.x, r);
+      int deg = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j >= g.maxdeg) break;  // uniform
+        const int y = r[j];
+        const bool ok = y >= 0 && y != v;
+        const uint32_t ly = L(ok ? y : h.x);
+        deg += y >= 0 ? 1 : 0;
+        h.has_v = h.has_v || y == v;
+        h.bits |= ok ? 1ull << ly : 0ull;
+        h.cnt += (ok && ly != h.lx) ? 1u : 0u;
+      }
+      h.deg = deg;
+      return h;
     } else {
       const int e0 = g.rowptr[v];
       dv = g.rowptr[v + 1] - e0;
@@ -438,21 +461,6 @@ struct Ctx {
       h.lx = L(h.x);
       const int f0 = g.rowptr[h.x], f1 = g.rowptr[h.x + 1];
       h.deg = f1 - f0;
-      if constexpr (E16) {
-        int r[16];
-        row16(h.x, r);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          if (j >= g.maxdeg) break;  // uniform
-          const int y = r[j];
-          const bool ok = y >= 0 && y != v;
-          const uint32_t ly = L(ok ? y : h.x);
-          h.has_v = h.has_v || y == v;
-          h.bits |= ok ? 1ull << ly : 0ull;
-          h.cnt += (ok && ly != h.lx) ? 1u : 0u;
-        }
-        return h;
-      }
       for (int e = f0; e < f1; ++e) {
         const int y = g.col[e];
         if (y == v) {
@@ -551,7 +559,15 @@ struct Ctx {
         const uint32_t o = act ? L(x) - (uint32_t)k : 0u;
         int xr = 0, xc = 0;
         int dmax = 0;
-        if (act) {
+        int r16[16];
+        if constexpr (E16) {
+          if (act) {
+            row16(x, r16);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dmax += r16[j] >= 0 ? 1 : 0;
+            my_deg += (uint32_t)dmax;
+          }
+        } else if (act) {
           if constexpr (GRID) divmod(x, xr, xc);
           dmax = GRID ? 4 : g.rowptr[x + 1] - g.rowptr[x];
           my_deg += (uint32_t)degree(x, xr, xc);
@@ -563,10 +579,6 @@ struct Ctx {
 #pragma unroll
           for (int d = 32; d >= 1; d >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, d, WAVE));
           jmax = (int)rfl(dm);
-        }
-        int r16[16];
-        if constexpr (E16) {
-          if (act) row16(x, r16);
         }
         for (int j = 0; j < (E16 ? 16 : 64); ++j) {  // r16[j]: uniform j (v_movrels)
           if (j >= jmax) break;  // uniform
@@ -656,7 +668,8 @@ struct Ctx {
     if constexpr (!GRID) {
       // sources joined by a direct edge form one local component (the same links as the
       // oracle's contiguous_after): one component is connected; otherwise pre-merge
-      const int e0 = g.rowptr[v];
+      // nbadj has the padded [n][16] layout whenever the padded table exists
+      const size_t e0 = (E16 || g.ell) ? (size_t)v * 16 : (size_t)g.rowptr[v];
       const uint64_t adjl = ((am >> lane) & 1ull) ? (g.nbadj[e0 + lane - 1] << 1) & am : 0ull;
       uint64_t comp = am & (~am + 1ull);  // the lowest source
       for (;;) {
