@@ -67,6 +67,7 @@ SIGNATURES = [
     ("fw_chains_read", ctypes.c_int, [_P, _I32, _P, ctypes.c_size_t]),
     ("fw_chains_reset_observables", ctypes.c_int, [_P]),
     ("fw_chains_set_accept", ctypes.c_int, [_P, _I32, _P]),
+    ("fw_chains_set_schedule", ctypes.c_int, [_P, _P, _I32, _I64]),
     ("fw_chains_enable_maps", ctypes.c_int, [_P, _P]),
     ("fw_chains_read_map", ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, ctypes.c_size_t]),
     ("fw_eval_flips", ctypes.c_int,

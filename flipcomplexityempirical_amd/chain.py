@@ -54,6 +54,34 @@ def annealing_table(base: float, beta: float, maxdeg: int) -> np.ndarray:
     return np.array([b ** (beta * (-d)) for d in range(-maxdeg, maxdeg + 1)], dtype=np.float64)
 
 
+def reference_beta(t: int):
+    """The commented beta schedule of annealing_cut_accept_backwards
+    (grid_chain_sec11.py:88-93) at step_num t: 0 before 100,000, a linear ramp to 3 at
+    400,000, then 3 (Python int / float values as the reference writes them)."""
+    if t < 100000:
+        return 0
+    if t < 400000:
+        return (t - 100000) / 100000
+    return 3
+
+
+def schedule_rows(base: float, beta_of_t, t_start: int, t_stop: int,
+                  maxdeg: int) -> tuple[np.ndarray, int]:
+    """Rows for ``Chains.set_schedule``: row i = annealing_table(base, beta_of_t(t_start+i))
+    for step_num t_start..t_stop; returns (rows, t0 = t_start).  Exact when beta_of_t is
+    constant for t <= t_start and for t >= t_stop (the kernel clamps to the end rows).
+    Each power is CPython's float pow, as in the reference."""
+    rows = np.empty((t_stop - t_start + 1, 2 * maxdeg + 1), np.float64)
+    cache = {}
+    for i in range(rows.shape[0]):
+        beta = beta_of_t(t_start + i)
+        key = (type(beta), beta)
+        if key not in cache:
+            cache[key] = annealing_table(base, beta, maxdeg)
+        rows[i] = cache[key]
+    return rows, t_start
+
+
 ACCEPT_RULES = {"cut": _lib.ACCEPT_CUT, "bratio": _lib.ACCEPT_BRATIO,
                 "boundary": _lib.ACCEPT_BOUNDARY}
 
@@ -196,6 +224,20 @@ class Chains:
         r = ACCEPT_RULES[rule] if isinstance(rule, str) else int(rule)
         fl = None if node_flags is None else np.ascontiguousarray(node_flags, np.uint8)
         check(_lib.load().fw_chains_set_accept(self._h, r, ptr(fl)))
+
+    def set_schedule(self, rows=None, t0: int = 0) -> None:
+        """Step-dependent bounds shared by every chain (fw_chains_set_schedule): a proposal
+        with step_num t (accepted flips + 1, grid_chain_sec11.py:282-289) uses row
+        clamp(t - t0, 0, len(rows) - 1) in place of the thr table.  ``rows=None`` removes
+        it.  See ``schedule_rows``."""
+        if rows is None:
+            check(_lib.load().fw_chains_set_schedule(self._h, None, 0, 0))
+            return
+        r = np.ascontiguousarray(rows, np.float64)
+        if r.ndim != 2 or r.shape[1] != self.thr.shape[-1]:
+            raise ValueError(f"schedule rows must be [n][{self.thr.shape[-1]}]")
+        self._sched = r
+        check(_lib.load().fw_chains_set_schedule(self._h, ptr(r), r.shape[0], int(t0)))
 
     # ------------------------------------------------------------- spatial maps
     def enable_maps(self, label_values: Optional[Sequence[int]] = None) -> None:

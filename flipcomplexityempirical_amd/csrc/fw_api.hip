@@ -136,9 +136,19 @@ struct fw_chains {
   // FW_ACCEPT_BOUNDARY
   uint8_t* d_flags = nullptr;
   int32_t* d_bcnt = nullptr;
+  // fw_chains_set_schedule
+  double* d_sched = nullptr;
+  uint64_t* d_sched53 = nullptr;
 };
 
 namespace {
+
+// integer form of a Metropolis bound: CPython's u = M * 2^-53 with integer M < 2^53,
+// so u < thr <=> M < thr * 2^53 (exact scaling) <=> M < ceil(thr * 2^53)
+uint64_t thr53_of(double thr) {
+  const double t = thr * 9007199254740992.0;
+  return !(t > 0.0) ? 0ull : (t >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)std::ceil(t));
+}
 
 // Label bits per node for a (k, maxdeg): the search marks visited nodes with codes
 // k..k+deg-1 and v with the all-ones value, so k + maxdeg must stay below it.
@@ -217,7 +227,7 @@ extern "C" {
 
 const char* fw_last_error(void) { return g_err.c_str(); }
 
-int32_t fw_version(void) { return 0x000200; }
+int32_t fw_version(void) { return 0x000300; }
 
 int32_t fw_device_count(void) {
   int c = 0;
@@ -377,7 +387,7 @@ void fw_chains_destroy(fw_chains* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_thr53, c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
-                  c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt};
+                  c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt, c->d_sched, c->d_sched53};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -488,13 +498,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     return fail(FW_EHIP, "occupancy query failed (LDS %d B)", use16 ? p.lds16 : p.lds_bytes);
   }
   const size_t nthr = (size_t)(thr_per_chain ? n_chains : 1) * (2 * D + 1);
-  // integer form of the Metropolis bound: CPython's u = M * 2^-53 with integer M < 2^53,
-  // so u < thr <=> M < thr * 2^53 (exact scaling) <=> M < ceil(thr * 2^53)
   std::vector<uint64_t> thr53(nthr);
-  for (size_t i = 0; i < nthr; ++i) {
-    const double t = thr[i] * 9007199254740992.0;
-    thr53[i] = !(t > 0.0) ? 0ull : (t >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)std::ceil(t));
-  }
+  for (size_t i = 0; i < nthr; ++i) thr53[i] = thr53_of(thr[i]);
   bool ok = hipMalloc(&c->d_labels, packed.size()) == hipSuccess &&
             hipMalloc(&c->d_stats, sizeof(fw_chain_stats) * n_chains) == hipSuccess &&
             hipMalloc(&c->d_pops, sizeof(int64_t) * pops.size()) == hipSuccess &&
@@ -699,6 +704,35 @@ int fw_chains_set_accept(fw_chains* c, int32_t rule, const uint8_t* node_flags) 
       return fail(FW_EHIP, "flag count init failed");
   }
   c->p.accept = rule;
+  return FW_OK;
+}
+
+int fw_chains_set_schedule(fw_chains* c, const double* rows, int32_t n_rows, int64_t t0) {
+  if (!c) return fail(FW_EINVAL, "null handle");
+  if (n_rows < 0 || (n_rows > 0 && !rows)) return fail(FW_EINVAL, "bad schedule rows");
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->d_sched) (void)hipFree(c->d_sched);
+  if (c->d_sched53) (void)hipFree(c->d_sched53);
+  c->d_sched = nullptr;
+  c->d_sched53 = nullptr;
+  c->p.sched = nullptr;
+  c->p.sched53 = nullptr;
+  c->p.sched_rows = 0;
+  c->p.sched_t0 = 0;
+  if (n_rows == 0) return FW_OK;
+  const size_t m = (size_t)n_rows * (2 * c->g->maxdeg + 1);
+  std::vector<uint64_t> r53(m);
+  for (size_t i = 0; i < m; ++i) r53[i] = thr53_of(rows[i]);
+  if (hipMalloc(&c->d_sched, sizeof(double) * m) != hipSuccess ||
+      hipMalloc(&c->d_sched53, sizeof(uint64_t) * m) != hipSuccess)
+    return fail(FW_ENOMEM, "schedule of %d rows", n_rows);
+  HIPCHK(hipMemcpy(c->d_sched, rows, sizeof(double) * m, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_sched53, r53.data(), sizeof(uint64_t) * m, hipMemcpyHostToDevice));
+  c->p.sched = c->d_sched;
+  c->p.sched53 = c->d_sched53;
+  c->p.sched_rows = n_rows;
+  c->p.sched_t0 = t0;
   return FW_OK;
 }
 

@@ -405,9 +405,20 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
     }
     int32_t pops = q < k ? (int32_t)p.pops[(size_t)cc * k + q] : 0;  // total pop < 2^31
-    const double thr_l = FULL && q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
-    const uint64_t thr53_l = q < 2 * D + 1 ? p.thr53[(size_t)cc * p.thr_stride + q] : 0ull;
+    double thr_l = FULL && q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
+    uint64_t thr53_l = q < 2 * D + 1 ? p.thr53[(size_t)cc * p.thr_stride + q] : 0ull;
     fw_chain_stats* stp = p.stats + cc;
+    const uint64_t acc0 = FULL && p.sched ? stp->accepts : 0ull;
+    // scheduled bounds: the row of the next proposal's step_num (accepted flips + 1)
+    auto sched_row = [&](uint64_t nacc) {
+      const int64_t t = (int64_t)(acc0 + nacc) + 1 - p.sched_t0;
+      const int64_t r = t < 0 ? 0 : (t >= p.sched_rows ? p.sched_rows - 1 : t);
+      if (q < 2 * D + 1) {
+        thr_l = p.sched[r * (2 * D + 1) + q];
+        thr53_l = p.sched53[r * (2 * D + 1) + q];
+      }
+    };
+    if (FULL && p.sched) sched_row(0);
     uint64_t attempts = stp->attempts;
     const uint64_t yields0 = stp->yields;
     int32_t stuck = has ? stp->stuck : 1;
@@ -791,6 +802,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const int dnp = (int)row_sum(accepted && mine ? wn - wo : 0u);
       if (accepted) {
         n_acc += 1;
+        if (FULL && p.sched) sched_row(n_acc);
         n_adeg += (uint32_t)dv;
         npairs += dnp;
         cut += dcut;
@@ -887,7 +899,7 @@ bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop) {
 }
 
 void* fw_grid16_fn(const FwRunParams& p) {
-  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT;
+  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr;
   return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
 }
 

@@ -35,6 +35,12 @@ struct FwRunParams {
   const uint64_t* thr53;       // same shape: ceil(thr * 2^53) clamped to 2^53 (u < thr <=>
                                // u * 2^53 < thr53 for CPython's 53-bit u)
   int32_t thr_stride;          // 0 (shared table) or 2*maxdeg+1
+  // threshold schedule (fw_chains_set_schedule): when set, a proposal whose step_num
+  // (accepted flips so far + 1) is t uses row clamp(t - sched_t0, 0, sched_rows - 1)
+  const double* sched;         // [sched_rows][2*maxdeg+1] or null
+  const uint64_t* sched53;     // the same rows in the integer form of thr53
+  int64_t sched_t0;
+  int32_t sched_rows;
   unsigned long long* hist_cut;  // [nedges+1+FW_HIST_PAD]
   unsigned long long* hist_b;    // [n+1+FW_HIST_PAD]
   uint32_t* spill;             // [grid][n] search-list spill

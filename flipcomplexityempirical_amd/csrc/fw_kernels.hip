@@ -64,8 +64,16 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       for (int i = lane; i < p.lab_bytes / 16; i += WAVE) dst[i] = src[i];
     }
     int64_t pops = lane < k ? p.pops[(size_t)c * k + lane] : 0;  // lane d holds district d
-    const double thr_l = lane < 2 * D + 1 ? p.thr[(size_t)c * p.thr_stride + lane] : 0.0;
+    double thr_l = lane < 2 * D + 1 ? p.thr[(size_t)c * p.thr_stride + lane] : 0.0;
     fw_chain_stats* stp = p.stats + c;
+    const uint64_t acc0 = p.sched ? rfl64(stp->accepts) : 0ull;
+    // scheduled bounds: the row of the next proposal's step_num (accepted flips + 1)
+    auto sched_row = [&](uint64_t nacc) {
+      const int64_t t = (int64_t)(acc0 + nacc) + 1 - p.sched_t0;
+      const int64_t r = t < 0 ? 0 : (t >= p.sched_rows ? p.sched_rows - 1 : t);
+      if (lane < 2 * D + 1) thr_l = p.sched[r * (2 * D + 1) + lane];
+    };
+    if (p.sched) sched_row(0);
     uint64_t attempts = rfl64(stp->attempts);
     const uint64_t yields0 = rfl64(stp->yields);
     int32_t stuck = rfl(stp->stuck);
@@ -243,6 +251,7 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       }
       if (accepted) {
         n_acc += 1;
+        if (p.sched) sched_row(n_acc);
         n_adeg += (uint32_t)dv;
         if (lane == 0) PK<LB>::axor(C.lab, v, a ^ d);
         if (mine && h.x >= 0 && wn != wo) lds_add(C.gsum + (h.x >> 6), wn - wo);

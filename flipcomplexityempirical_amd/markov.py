@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _lib
 from .chain import (DEFAULT_MAX_RETRIES, Chains, DeviceGraph, RunResult, annealing_table,
-                    eval_flips, population_bounds, read_maps)
+                    eval_flips, population_bounds, read_maps, reference_beta, schedule_rows)
 from .graph import Graph, boundary_flags
 
 
@@ -292,8 +292,16 @@ class AnnealingCutAccept:
     """annealing_cut_accept_backwards with explicit base / beta (the reference fixes
     base = .1, beta = 5): random() < base**(beta*(c_old - c_new)) * |B'| / |B|."""
 
-    def __init__(self, base: float = 0.1, beta: float = 5):
-        self.base, self.beta = float(base), beta
+    def __init__(self, base: float = 0.1, beta: float = 5, schedule=None):
+        """``schedule`` = (beta_of_t, t_start, t_stop): beta as a function of
+        partition["step_num"], constant outside [t_start, t_stop] — e.g.
+        ``AnnealingCutAccept.reference_schedule()``, the reference's commented ramp."""
+        self.base, self.beta, self.schedule = float(base), beta, schedule
+
+    @classmethod
+    def reference_schedule(cls, base: float = 0.1) -> "AnnealingCutAccept":
+        """grid_chain_sec11.py:88-93: beta 0 until step 100,000, ramp to 3 at 400,000."""
+        return cls(base, 3, (reference_beta, 100000, 400000))
 
     def __call__(self, partition: Partition) -> bool:
         raise NotImplementedError("AnnealingCutAccept is lowered to the GPU kernel")
@@ -352,6 +360,7 @@ class MarkovChain:
         lo, hi = bounds[0].bounds
         self.pop_bounds = (int(math.ceil(lo)), int(math.floor(hi)))
         self.accept_rule, self.thr, self.flags = "cut", None, None
+        self.schedule = None
         if isinstance(accept, MetropolisCutAccept):
             self.base = accept.base
         elif isinstance(accept, AnnealingCutAccept) or \
@@ -359,6 +368,10 @@ class MarkovChain:
             a = accept if isinstance(accept, AnnealingCutAccept) else AnnealingCutAccept()
             self.base, self.accept_rule = a.base, "bratio"
             self.thr = annealing_table(a.base, a.beta, initial_state.graph.maxdeg)
+            if a.schedule is not None:
+                fn, t_start, t_stop = a.schedule
+                self.schedule = schedule_rows(a.base, fn, t_start, t_stop,
+                                              initial_state.graph.maxdeg)
         elif _fname(accept) == "uniform_accept":
             # boundary_condition reads partition["boundary"] (grid_chain_sec11.py:44), the
             # boundary_node nodes; without that updater the graph's attribute is used
@@ -390,6 +403,8 @@ class MarkovChain:
                     chain_id0=self.chain_id if chain_id0 is None else chain_id0, thr=self.thr)
         if self.accept_rule != "cut":
             ch.set_accept(self.accept_rule, self.flags)
+        if self.schedule is not None:
+            ch.set_schedule(*self.schedule)
         return ch
 
     def __iter__(self):

@@ -131,7 +131,8 @@ typedef struct fw_chains fw_chains;
 /* Thread-local description of the last error on this thread. */
 const char* fw_last_error(void);
 
-/* Library/ABI version, e.g. 0x000200 for 0.2.0 (0.2: spatial maps). */
+/* Library/ABI version, e.g. 0x000300 for 0.3.0 (0.2: spatial maps; 0.3: bound
+ * schedules). */
 int32_t fw_version(void);
 
 /* Number of visible HIP devices (0 when none; never fails). */
@@ -196,6 +197,16 @@ int fw_chains_reset_observables(fw_chains* c);
  * boundary_node) is required by FW_ACCEPT_BOUNDARY and ignored otherwise.  May be
  * called between runs. */
 int fw_chains_set_accept(fw_chains* c, int32_t rule, const uint8_t* node_flags);
+
+/* Step-dependent Metropolis bounds for FW_ACCEPT_CUT / FW_ACCEPT_BRATIO, shared by
+ * every chain: the commented beta schedule of annealing_cut_accept_backwards
+ * (grid_chain_sec11.py:85-93, t = partition["step_num"], the step_num updater
+ * :282-289 = flips accepted since the initial plan, + 1 for the proposal).  A
+ * proposal with step_num t uses row clamp(t - t0, 0, n_rows - 1) of rows
+ * [n_rows][2*maxdeg+1] in place of the chain's thr table (Δcut + maxdeg indexes
+ * a row, as for thr).  n_rows == 0 removes the schedule.  May be called between
+ * runs; the accepted-flip count is the FW_READ_STATS accepts field. */
+int fw_chains_set_schedule(fw_chains* c, const double* rows, int32_t n_rows, int64_t t0);
 
 /* Turn on the spatial observables for every chain (before the first run).
  * label_values [k] are the GerryChain assignment values of districts 0..k-1

@@ -112,6 +112,9 @@ typedef struct {
   uint64_t* hist_b;   /* may be NULL */
   struct orc_maps* maps; /* may be NULL */
   int32_t accept_rule;   /* FW_ACCEPT_* */
+  const double* sched;   /* fw_chains_set_schedule rows [sched_rows][2*maxdeg+1] or NULL */
+  int32_t sched_rows;
+  int64_t sched_t0;
   const uint8_t* flags;  /* [n] boundary_node flags (FW_ACCEPT_BOUNDARY), may be NULL */
   int64_t* bcnt;         /* [k] flagged nodes per district */
 } chain_t;
@@ -232,9 +235,15 @@ static int32_t bnodes_after(chain_t* c, int32_t v, int16_t b) {
  *                      districts, else u < 0 */
 static int accept_of(chain_t* c, int32_t v, int16_t b, int32_t dcut, double u) {
   const int32_t D = c->g.maxdeg;
+  const double* thr = c->thr;
+  if (c->sched) { /* step_num of the proposal (grid_chain_sec11.py:282-289) = accepts + 1 */
+    const int64_t t = (int64_t)c->st.accepts + 1 - c->sched_t0;
+    const int64_t r = t < 0 ? 0 : (t >= c->sched_rows ? c->sched_rows - 1 : t);
+    thr = c->sched + r * (2 * D + 1);
+  }
   if (c->accept_rule == FW_ACCEPT_BRATIO) {
     const double ratio = (double)bnodes_after(c, v, b) / (double)c->st.bnodes;
-    return u < c->thr[dcut + D] * ratio;
+    return u < thr[dcut + D] * ratio;
   }
   if (c->accept_rule == FW_ACCEPT_BOUNDARY) {
     const int64_t fv = c->flags && c->flags[v] ? 1 : 0;
@@ -246,7 +255,7 @@ static int accept_of(chain_t* c, int32_t v, int16_t b, int32_t dcut, double u) {
     }
     return u < (parts >= 2 ? 1.0 : 0.0);
   }
-  return u < c->thr[dcut + D];
+  return u < thr[dcut + D];
 }
 
 /* --- contiguity: exact verdict + the same level-synchronous race search the
@@ -567,7 +576,8 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
                      const double* thr, uint64_t seed, uint64_t chain_id, int16_t* labels,
                      fw_chain_stats* stats, int64_t steps, int32_t max_retries,
                      uint64_t* hist_cut, uint64_t* hist_b, int32_t* trace, int64_t* pops_out,
-                     orc_maps* maps, int32_t accept_rule, const uint8_t* flags) {
+                     orc_maps* maps, int32_t accept_rule, const uint8_t* flags,
+                     const double* sched, int32_t sched_rows, int64_t sched_t0) {
   chain_t c;
   if (setup(&c, rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr)) {
     teardown(&c);
@@ -582,6 +592,9 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
   c.maps = maps;
   c.accept_rule = accept_rule;
   c.flags = flags;
+  c.sched = sched_rows > 0 ? sched : NULL;
+  c.sched_rows = sched_rows;
+  c.sched_t0 = sched_t0;
   derive(&c);
     if (c.st.yields == 0 && c.st.attempts == 0) yield_obs(&c);
   for (int64_t s = 0; s < steps && !c.st.stuck; ++s) {
@@ -649,7 +662,7 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
                   uint64_t* hist_b, int32_t* trace, int64_t* pops_out) {
   return orc_run_chain_ex(rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr, seed,
                           chain_id, labels, stats, steps, max_retries, hist_cut, hist_b, trace,
-                          pops_out, NULL, FW_ACCEPT_CUT, NULL);
+                          pops_out, NULL, FW_ACCEPT_CUT, NULL, NULL, 0, 0);
 }
 
 /* Per-flip evaluation on one state (the fw_eval_flips contract). */

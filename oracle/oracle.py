@@ -65,7 +65,8 @@ def lib():
             ctypes.c_int64, ctypes.c_int32, _P, _P, _P, _P,
         ]
         L.orc_run_chain.restype = ctypes.c_int
-        L.orc_run_chain_ex.argtypes = L.orc_run_chain.argtypes + [_P, ctypes.c_int32, _P]
+        L.orc_run_chain_ex.argtypes = L.orc_run_chain.argtypes + [
+            _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int64]
         L.orc_run_chain_ex.restype = ctypes.c_int
         L.orc_eval_flips.argtypes = [
             _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
@@ -131,14 +132,18 @@ class Maps:
 
 def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps,
               max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False,
-              maps=None, accept_rule=0, flags=None):
+              maps=None, accept_rule=0, flags=None, schedule=None):
     """Run one chain on the CPU oracle.  ``graph`` needs rowptr/col/pop/n/grid_w.
 
     Returns (labels, stats, pops, trace-or-None); ``labels`` is a new int16 array.
     ``maps`` (an oracle ``Maps``) accumulates the per-yield spatial observables;
     ``accept_rule`` is FW_ACCEPT_* (0 cut_accept, 1 the |B'|/|B| rule, 2 uniform_accept
-    with boundary_condition over the uint8 ``flags``).
+    with boundary_condition over the uint8 ``flags``).  ``schedule`` = (rows, t0): the
+    step-dependent bounds of fw_chains_set_schedule.
     """
+    srows, st0 = (None, 0) if schedule is None else schedule
+    if srows is not None:
+        srows = np.ascontiguousarray(srows, np.float64)
     fl = None if flags is None else np.ascontiguousarray(flags, np.uint8)
     lab = np.array(labels, dtype=np.int16, copy=True)
     st = new_stats(1) if stats is None else stats
@@ -150,6 +155,7 @@ def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps
         int(pop_lo), int(pop_hi), _ptr(thr), int(seed), int(chain_id), _ptr(lab), _ptr(st),
         int(steps), int(max_retries), _ptr(hist_cut), _ptr(hist_b), _ptr(tr), _ptr(pops),
         None if maps is None else ctypes.byref(maps._s), int(accept_rule), _ptr(fl),
+        _ptr(srows), 0 if srows is None else int(srows.shape[0]), int(st0),
     )
     if rc != 0:
         raise MemoryError("oracle allocation failed")

@@ -150,8 +150,16 @@ def b_nodes(partition):
         {(x[1], a[x[0]]) for x in partition["cut_edges"]})
 
 
+def step_num(partition):
+    """grid_chain_sec11.py:282-289: 0 for the initial plan, else the parent's + 1."""
+    parent = partition.parent
+    if not parent:
+        return 0
+    return parent["step_num"] + 1
+
+
 UPDATERS = {"cut_edges": cut_edges, "population": population, "b_nodes_bi": b_nodes_bi,
-            "b_nodes": b_nodes}
+            "b_nodes": b_nodes, "step_num": step_num}
 
 
 # ----------------------------------------------------------------- proposals
@@ -211,7 +219,11 @@ class PopBound:
 # ----------------------------------------------------------------- accept rules
 def annealing_cut_accept_bound(partition, base, beta):
     """annealing_cut_accept_backwards, grid_chain_sec11.py:81-110 (its bound; the Validator
-    already enforced its inline popbound / single_flip_contiguous checks)."""
+    already enforced its inline popbound / single_flip_contiguous checks).  A callable
+    ``beta`` is the commented schedule (:85-93): beta = beta(partition["step_num"])."""
+    t = partition["step_num"]
+    if callable(beta):
+        beta = beta(t)
     boundaries1 = {x[0] for x in partition["cut_edges"]}.union(
         {x[1] for x in partition["cut_edges"]})
     boundaries2 = {x[0] for x in partition.parent["cut_edges"]}.union(

@@ -175,3 +175,37 @@ def test_alternative_accepts_through_the_facade(gpu_lib, accept):
                                       accept_rule=1 if accept == "annealing" else 2, flags=flags)
         assert np.array_equal(res.labels[i], olab)
         assert res.stats["accepts"][i] == ost["accepts"][0]
+
+
+def test_reference_beta_schedule_is_lowered():
+    """AnnealingCutAccept.reference_schedule() (grid_chain_sec11.py:88-93) lowers to
+    FW_ACCEPT_BRATIO with step_num-indexed rows (host side only; the kernels are checked
+    in tests/test_gpu_parity.py::test_step_schedule_bit_exact)."""
+    from flipcomplexityempirical_amd.chain import annealing_table
+    g, part = sec11_partition()
+    pb = gc.within_percent_of_ideal_population(part, 0.05)
+    chain = gc.MarkovChain(gc.slow_reversible_propose_bi, [gc.single_flip_contiguous, pb],
+                           gc.AnnealingCutAccept.reference_schedule(), part, 10)
+    rows, t0 = chain.schedule
+    assert chain.accept_rule == "bratio" and t0 == 100000 and rows.shape == (300001, 9)
+    assert np.array_equal(rows[200000], annealing_table(0.1, 2.0, 4))
+
+
+@pytest.mark.gpu
+def test_scheduled_annealing_through_the_facade(gpu_lib):
+    """A step_num schedule through the façade equals the oracle with the same rows."""
+    from flipcomplexityempirical_amd.chain import schedule_rows
+    g, part = sec11_partition(alignment=1, base=0.1)
+    pb = gc.within_percent_of_ideal_population(part, 0.10)
+    beta = lambda t: 0 if t < 50 else ((t - 50) / 100 if t < 250 else 2)  # noqa: E731
+    acc = gc.AnnealingCutAccept(0.1, 2, (beta, 50, 250))
+    chain = gc.MarkovChain(gc.slow_reversible_propose_bi, gc.Validator(
+        [gc.single_flip_contiguous, pb]), accept=acc, initial_state=part, total_steps=801, seed=4)
+    res = chain.run_batched(3, chain_id0=2)
+    lo, hi = population_bounds(g.n, 2, 0.10)
+    rows, t0 = schedule_rows(0.1, beta, 50, 250, 4)
+    for i in range(3):
+        olab, ost, _, _ = O.run_chain(g, sec11_seed(g, 1), 2, 0, lo, hi, rows[0], 4, 2 + i, 800,
+                                      accept_rule=1, schedule=(rows, t0))
+        assert np.array_equal(res.labels[i], olab)
+        assert res.stats["accepts"][i] == ost["accepts"][0]

@@ -239,3 +239,57 @@ def test_large_grid_ladder_bit_exact(gpu_lib, n, k, bw, monkeypatch):
                                          s, stats=ost)
         assert np.array_equal(labs[i], lab), i
         assert_stats_equal(st[i:i + 1], ost)
+
+
+def _ramp(t):
+    """A short stand-in for the reference's commented beta ramp (grid_chain_sec11.py:88-93)."""
+    if t < 40:
+        return 0
+    if t < 160:
+        return (t - 40) / 40
+    return 3
+
+
+SCHED_CASES = [("grid12_k4_pairs", "bratio", "auto"), ("grid20_k4_mu", "bratio", "wave64"),
+               ("sec11_a2_k2", "bratio", "auto"), ("tract_k4", "bratio", "auto"),
+               ("grid12_k4_cut", "cut", "auto"), ("grid30x18_k2_bi", "cut", "wave64")]
+
+
+@pytest.mark.parametrize("name,rule,path", SCHED_CASES,
+                         ids=[f"{p}-{r}-{n}" for n, r, p in SCHED_CASES])
+def test_step_schedule_bit_exact(gpu_lib, name, rule, path, monkeypatch):
+    """fw_chains_set_schedule: bounds indexed by step_num (accepted flips + 1) against the
+    oracle, across two runs (the schedule position carries over) and a schedule change."""
+    from flipcomplexityempirical_amd.chain import schedule_rows
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    g = case.graph
+    r = 1 if rule == "bratio" else 0
+    base = 0.1 if rule == "bratio" else 1.0 / max(case.base, 1e-9)
+    rows, t0 = schedule_rows(base, _ramp, 40, 160, g.maxdeg)
+    rows2, t02 = schedule_rows(base, lambda t: 2 - t / 200, 0, 400, g.maxdeg)
+    n_chains, seed, id0 = 7, 91, 5
+    dg = DeviceGraph(g)
+    ch = Chains(dg, n_chains, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                seed=seed, chain_id0=id0, thr=case.thr)
+    if rule == "bratio":
+        ch.set_accept(rule)
+    ch.set_schedule(rows, t0)
+    ch.run(150)
+    ch.run(250)
+    ch.set_schedule(rows2, t02)
+    ch.run(200)
+    labs, st = ch.labels(), ch.stats()
+    lo, hi = case.bounds
+    for i in range(n_chains):
+        lab, ost = case.init.copy(), O.new_stats(1)
+        for s, sch in ((150, (rows, t0)), (250, (rows, t0)), (200, (rows2, t02))):
+            lab, ost, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, case.thr, seed,
+                                         id0 + i, s, stats=ost, accept_rule=r, schedule=sch)
+        assert np.array_equal(labs[i], lab), (name, i)
+        for f in ("attempts", "steps", "accepts", "sum_cut", "bnodes"):
+            assert st[f][i] == ost[f][0], (name, i, f)
+    assert st["accepts"].min() > 50  # the chains did move through the schedule

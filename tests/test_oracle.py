@@ -225,3 +225,45 @@ def test_accept_rules_follow_the_reference_functions(name, rule):
     for f in ("attempts", "steps", "accepts"):
         assert ch.counters[f] == int(st[f][0]), f
     assert 0 < st["accepts"][0] < S or rule == "boundary"
+
+
+def _ramp(t):
+    if t < 30:
+        return 0
+    if t < 130:
+        return (t - 30) / 50
+    return 2
+
+
+@pytest.mark.parametrize("name", ["grid10_k2_bi", "grid12_k4_pairs", "sec11_a2_k2"])
+def test_beta_schedule_follows_step_num(name):
+    """Oracle schedule rows (fw_chains_set_schedule) == the proxy evaluating
+    annealing_cut_accept_backwards with beta = f(partition["step_num"]), the reference's
+    commented schedule form (grid_chain_sec11.py:85-93, step_num :282-289)."""
+    from flipcomplexityempirical_amd.chain import schedule_rows
+    case = CASES[name]
+    g = case.graph
+    S = 700
+    rows, t0 = schedule_rows(0.1, _ramp, 30, 130, g.maxdeg)
+    lab, st, _, _ = O.run_chain(g, case.init, case.k, case.mode, *case.bounds, rows[0], 17, 3,
+                                S, accept_rule=1, schedule=(rows, t0))
+    ch = ProxyChain(g, case.init, case.k, case.mode, case.percent, 0.1, 17, 3, accept="bratio",
+                    beta=_ramp)
+    ch.run(S, bounds=case.bounds)
+    assert np.array_equal(np.array(ch.labels()), lab)
+    for f in ("attempts", "steps", "accepts"):
+        assert ch.counters[f] == int(st[f][0]), f
+    assert st["accepts"][0] > 130  # the run went past the end of the ramp
+
+
+def test_reference_beta_schedule_rows():
+    """reference_beta is the commented ramp (grid_chain_sec11.py:88-93); its rows are exact
+    at both clamped ends."""
+    from flipcomplexityempirical_amd.chain import annealing_table, reference_beta, schedule_rows
+    assert reference_beta(99999) == 0 and reference_beta(100000) == 0.0
+    assert reference_beta(250000) == 1.5 and reference_beta(400000) == 3
+    rows, t0 = schedule_rows(0.1, reference_beta, 100000, 400000, 4)
+    assert t0 == 100000 and rows.shape == (300001, 9)
+    assert np.array_equal(rows[0], annealing_table(0.1, 0, 4))
+    assert np.array_equal(rows[-1], annealing_table(0.1, 3, 4))
+    assert np.array_equal(rows[150000], annealing_table(0.1, 1.5, 4))
