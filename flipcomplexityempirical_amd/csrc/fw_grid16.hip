@@ -451,6 +451,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         }
         if (q == 0 && has) gsum[t2] = tot[0] | (tot[1] << 16);
       }
+      // zero padding up to 16 lanes x PER/2 words: level 1 reads every word unmasked
+      for (int t2 = GW + q; t2 < 8 * PER; t2 += ROW)
+        if (has) gsum[t2] = 0u;
       cut = (int32_t)(row_sum(cut2) / 2);
       bnodes = (int32_t)row_sum(bn);
       npairs = (int32_t)row_sum(np);
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 #pragma unroll
       for (int t = 0; t < PER / 2; ++t) {
         const int wi = q * (PER / 2) + t;
-        const uint32_t w2 = wi < GW ? gsum[wi] : 0u;
+        const uint32_t w2 = gsum[wi];  // words past GW are zero padding
         gs[2 * t] = w2 & 0xFFFFu;
         gs[2 * t + 1] = w2 >> 16;
         s += gs[2 * t] + gs[2 * t + 1];
@@ -860,12 +863,17 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   STAMP_FLUSH
 }
 
+// group sums per lane (PER) for G groups
+int per16(int G) { return G <= 16 * 2 ? 2 : G <= 16 * 4 ? 4 : G <= 16 * 10 ? 10 : 16; }
+
 template <int LB, int MODE, bool FULL>
 void* pick16(int G) {
-  if (G <= 16 * 2) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL>);
-  if (G <= 16 * 4) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL>);
-  if (G <= 16 * 10) return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL>);
-  return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL>);
+  switch (per16(G)) {
+    case 2: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL>);
+    case 4: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL>);
+    case 10: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL>);
+    default: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL>);
+  }
 }
 
 template <bool FULL>
@@ -908,7 +916,7 @@ void* fw_grid16_fn(const FwRunParams& p) {
 // 4-bit search scratch and visit list.  Picks the waves per workgroup (1..4) that keep
 // the most chains resident per CU (ties: fewer waves).
 int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
-  const int slot = round16i(p.lab_bytes + 4 * ((p.G + 1) / 2));
+  const int slot = round16i(p.lab_bytes) + 4 * 8 * per16(p.G);  // + u16 sums, 16 x PER
   int stride = slot;
   while (stride % 128 != 16) stride += 16;
   p.slot_stride = stride;
