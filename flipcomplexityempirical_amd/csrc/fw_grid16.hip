@@ -98,7 +98,8 @@ __device__ __forceinline__ uint32_t lab_window(const LDS uint8_t* lab, int x) {
   const int bit = (x - 1) * LB;  // x - 1 may be -1: field 0 is then garbage, masked by callers
   const int wi = bit >> 5;       // arithmetic shift: -1 -> -1
   const LDS uint32_t* w = reinterpret_cast<const LDS uint32_t*>(lab);
-  const uint32_t lo = wi >= 0 ? w[wi] : 0u;
+  const uint32_t lo0 = w[wi > 0 ? wi : 0];  // unconditional read: no exec-mask branch
+  const uint32_t lo = wi >= 0 ? lo0 : 0u;
   const uint32_t hi = w[wi + 1];
   const uint64_t both = ((uint64_t)hi << 32) | lo;
   return (uint32_t)(both >> (uint32_t)(bit - wi * 32)) & ((1u << (6 * LB)) - 1u);
@@ -177,10 +178,14 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
                                               uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
   w4 = 0;
   cd4 = 0;
-  if (x0 >= n) return;
-  const uint32_t own = lab_window<2>(lab, x0);  // fields x0-1 .. x0+4
-  const uint32_t up = x0 + 3 - W >= 0 ? lab_window<2>(lab, x0 - W) : 0u;
-  const uint32_t dn = x0 + W < n ? lab_window<2>(lab, x0 + W) : 0u;
+  // branch-free: every read is issued at a valid position and its result masked (mN is
+  // all-zero for a group tail past n)
+  const int xs = x0 < n ? x0 : 0;
+  const bool hasU = xs + 3 - W >= 0, hasD = xs + W < n;
+  const uint32_t own = lab_window<2>(lab, xs);  // fields x0-1 .. x0+4
+  const uint32_t up0 = lab_window<2>(lab, hasU ? xs - W : xs);
+  const uint32_t dn0 = lab_window<2>(lab, hasD ? xs + W : xs);
+  const uint32_t up = hasU ? up0 : 0u, dn = hasD ? dn0 : 0u;
   const uint32_t o_lo = onehot4(spread4(own)), o_hi = onehot4(spread4(own >> 8));
   const uint32_t L = o_lo;                                     // x-1
   const uint32_t O = __builtin_amdgcn_alignbyte(o_hi, o_lo, 1);  // x
