@@ -362,7 +362,11 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   using P = PK<LB>;
   const int lane = __lane_id(), row = lane >> 4, q = lane & 15;
   const int wv = (int)(threadIdx.x >> 6);
-  const int W = p.g.gw, H = p.g.gh, n = p.g.n, D = p.g.maxdeg, G = p.G, k = p.k;
+  // grid shape and bounds live in VGPRs: the hot loop uses them only in vector ops, and
+  // the scalar file is the scarce one (SGPR spills cost v_readlane round trips)
+  const int W = (int)in_vgpr((uint32_t)p.g.gw), H = (int)in_vgpr((uint32_t)p.g.gh);
+  const int n = (int)in_vgpr((uint32_t)p.g.n);
+  const int D = p.g.maxdeg, G = p.G, k = p.k;
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
   LDS uint8_t* const lab = sm + (wv * 4 + row) * p.slot_stride;  // this row's chain slot
   LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);  // u16 pairs
@@ -374,13 +378,14 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   const bool maps_on = FULL && p.m_acc != nullptr;
   // population bounds as int32 (the host routes graphs with total population >= 2^31 to
   // the one-chain-per-wave kernel); clamped so comparisons keep their meaning
-  const int32_t pop_lo = (int32_t)max(p.pop_lo, (int64_t)INT32_MIN);
-  const int32_t pop_hi = (int32_t)min(p.pop_hi, (int64_t)INT32_MAX);
+  const int32_t pop_lo = (int32_t)in_vgpr((uint32_t)(int32_t)max(p.pop_lo, (int64_t)INT32_MIN));
+  const int32_t pop_hi = (int32_t)in_vgpr((uint32_t)(int32_t)min(p.pop_hi, (int64_t)INT32_MAX));
+  const uint32_t gm32 = in_vgpr(p.g.gm32);
   const int32_t rule = FULL ? p.accept : FW_ACCEPT_CUT;
   int my_dr, my_dc;
   role_off(q <= 8 ? q : 0, my_dr, my_dc);
   auto divmod = [&](int x, int& r, int& c) {
-    r = (int)__umulhi((uint32_t)x, p.g.gm32);
+    r = (int)__umulhi((uint32_t)x, gm32);
     c = x - r * W;
   };
   STAMP_DECL
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
-      weights4x<LB, MODE, false>(lab, x0, W, H, n, p.g.gm32, w4, cd4);
+      weights4x<LB, MODE, false>(lab, x0, W, H, n, gm32, w4, cd4);
       const uint32_t pref = w4 * 0x01010101u;  // byte t: weights of nodes 0..t (<= 16)
       const uint32_t ws = pref >> 24;
       const uint32_t incl2 = row_scan(ws);
