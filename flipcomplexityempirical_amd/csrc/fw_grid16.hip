@@ -366,7 +366,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   // the scalar file is the scarce one (SGPR spills cost v_readlane round trips)
   const int W = (int)in_vgpr((uint32_t)p.g.gw), H = (int)in_vgpr((uint32_t)p.g.gh);
   const int n = (int)in_vgpr((uint32_t)p.g.n);
-  const int D = p.g.maxdeg, G = p.G, k = p.k;
+  const int D = (int)in_vgpr((uint32_t)p.g.maxdeg), G = (int)in_vgpr((uint32_t)p.G);
+  const int k = (int)in_vgpr((uint32_t)p.k);
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
   LDS uint8_t* const lab = sm + (wv * 4 + row) * p.slot_stride;  // this row's chain slot
   LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);  // u16 pairs
