@@ -234,6 +234,29 @@ __device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
   return r;
 }
 
+// window_verdict (fw_device.h, = the oracle's orc_window_verdict) with the four source
+// flood fills run side by side in row-lanes 0..3 instead of one after another.  Fills
+// of sources in one window component are equal and other fills disjoint, so the
+// sequential verdict is order-free: 1 if some fill holds every source, else 0 if some
+// fill touches no border, else -1 (undecided).  Row-uniform result.
+__device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bool need) {
+  const uint64_t C0 = 0x0040810204081ull, C6 = C0 << 6;
+  const uint64_t BORDER = C0 | C6 | 0x7Full | (0x7Full << 42);
+  const uint64_t src = A & ((1ull << 17) | (1ull << 23) | (1ull << 25) | (1ull << 31));
+  const int sb = q == 0 ? 17 : q == 1 ? 23 : q == 2 ? 25 : 31;
+  uint64_t x = (need && q < 4) ? src & (1ull << sb) : 0ull;
+  if (x) {
+    for (;;) {
+      const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
+      if (y == x) break;
+      x = y;
+    }
+  }
+  const uint32_t full = rowbits(ballot(x != 0ull && (x & src) == src), row);
+  const uint32_t closed = rowbits(ballot(x != 0ull && (x & BORDER) == 0ull), row);
+  return full ? 1 : (closed ? 0 : -1);
+}
+
 // 4-bit scratch field x := 0 (atomic on the shared word)
 __device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
   __atomic_fetch_and(PK<4>::word(scr, x), ~(15u << PK<4>::shift(x)), __ATOMIC_RELAXED);
@@ -668,14 +691,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (ballot(need)) {  // 7x7 window flood fill (3 window cells per row-lane)
         uint64_t A = 0;
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
+        for (int t = 0; t < 3; ++t) {  // branch-free: clamped read, masked result
           const int pos = window_pos(q + ROW * t);
           const int rr = vr - 3 + pos / 7, cw = vc - 3 + pos % 7;
-          const bool in = rr >= 0 && rr < H && cw >= 0 && cw < W && P::get(lab, rr * W + cw) == a;
-          A |= (uint64_t)rowbits(ballot(in), row) << (ROW * t);
+          const bool inb = rr >= 0 && rr < H && cw >= 0 && cw < W;
+          const uint32_t lw = P::get(lab, inb ? rr * W + cw : v);
+          A |= (uint64_t)rowbits(ballot(inb && lw == a), row) << (ROW * t);
         }
         A = (A & ((1ull << 24) - 1ull)) | ((A >> 24) << 25);
-        const int wvd = need ? window_verdict(A) : -1;
+        const int wvd = window_verdict_row(A, q, row, need);
         if (wvd >= 0) {
           contig = wvd == 1;
           need = false;
