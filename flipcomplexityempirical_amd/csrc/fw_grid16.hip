@@ -87,7 +87,9 @@ __device__ __forceinline__ uint32_t row_shl1(uint32_t x) {
 }
 // value held by row-lane L (row-uniform L in 0..15; anything else gives 0)
 __device__ __forceinline__ uint32_t row_pick(uint32_t x, int L, int q) {
-  return row_sum(q == L ? x : 0u);
+  // one LDS-crossbar permute instead of a four-step DPP row sum
+  const int src = ((__lane_id() - q) + L) << 2;
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)x);
 }
 
 // Labels of the six consecutive nodes x-1 .. x+4 of a packed LB-bit label array, LB
@@ -648,7 +650,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           }
         }
       }
-      const uint32_t a = row_pick(h.lx, 0, q);
+      const uint32_t a = row_first(h.lx);  // v's label (row-lane 0)
       const bool isnb = q >= 1 && q <= 4 && h.x >= 0;
       uint32_t d;
       if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
