@@ -38,6 +38,16 @@ __device__ __forceinline__ uint32_t rdl(uint32_t x, int l) {
 __device__ __forceinline__ int32_t rdl(int32_t x, int l) {
   return (int32_t)__builtin_amdgcn_readlane((uint32_t)x, l);
 }
+// Launders a wave-uniform value into a VGPR (keeps it out of the scarce SGPRs; the
+// volatile asm is not hoisted, so per-use copies are not turned back into SGPR constants)
+__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+__device__ __forceinline__ uint64_t in_vgpr64(uint64_t x) {
+  return ((uint64_t)in_vgpr((uint32_t)(x >> 32)) << 32) | in_vgpr((uint32_t)x);
+}
 __device__ __forceinline__ uint64_t rdl64(uint64_t x, int l) {
   uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
   uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);

@@ -228,13 +228,6 @@ __device__ __forceinline__ void weights4x(const LDS uint8_t* lab, int x0, int W,
 // bytes of w (each < 64) summed
 __device__ __forceinline__ uint32_t bsum4m(uint32_t v) { return (v * 0x01010101u) >> 24; }
 
-// Launders a wave-uniform value into a VGPR (keeps it out of the scarce SGPRs; the
-// volatile asm is not hoisted, so per-use copies are not turned back into SGPR constants)
-__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
-  uint32_t r;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
-  return r;
-}
 
 // window_verdict (fw_device.h, = the oracle's orc_window_verdict) with the four source
 // flood fills run side by side in row-lanes 0..3 instead of one after another.  Fills

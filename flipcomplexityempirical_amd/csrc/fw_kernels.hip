@@ -30,7 +30,7 @@ namespace {
 
 // ---------------------------------------------------------------- the chain kernel
 template <int LB, bool GRID, int MODE, int PER, bool E16>
-__global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void fw_run_kernel(FwRunParams p) {
   extern __shared__ __align__(16) uint8_t smem[];
   Ctx<LB, GRID, E16> C;
   C.g = p.g;
@@ -80,10 +80,11 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
     int64_t sum_cut = (int64_t)rfl64((uint64_t)stp->sum_cut);
     int64_t sum_bnodes = (int64_t)rfl64((uint64_t)stp->sum_bnodes);
     double sum_invb = stp->sum_invb;  // running total: keeps the oracle's summation order
-    // per-launch counters (added to the 64-bit totals at the end)
-    uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0;
-    uint32_t n_sdeg = 0, n_adeg = 0, n_bchg = 0, n_yield = 0;
-    uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
+    // per-launch counters (added to the 64-bit totals at the end), held in VGPRs: the
+    // chain's uniform state already fills the scalar file
+    uint32_t n_steps = in_vgpr(0), n_acc = in_vgpr(0), n_popf = in_vgpr(0), n_conf = in_vgpr(0);
+    uint32_t n_sdeg = in_vgpr(0), n_adeg = in_vgpr(0), n_bchg = in_vgpr(0), n_yield = in_vgpr(0);
+    uint64_t n_bfs = in_vgpr64(0), n_bfsn = in_vgpr64(0), n_bfsd = in_vgpr64(0);
     Pend pend = pend_load(p, c);
     // boundary_node-flagged nodes of district `lane` (FW_ACCEPT_BOUNDARY)
     int32_t bcnt = p.accept == FW_ACCEPT_BOUNDARY && lane < k ? p.bcnt[(size_t)c * k + lane] : 0;
@@ -136,6 +137,10 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
       hb += (lane == ib);
     };
     if (yields0 == 0 && attempts == 0) observe();
+    // Philox batches on the VALU: lane l holds the draw of attempt (batch base + l); an
+    // attempt reads its four words with v_readlane (no scalar round-key table to spill)
+    U4 pb = {0u, 0u, 0u, 0u};
+    int bpos = WAVE;
 
     const bool unit_pop = p.g.pop == nullptr;
     for (int64_t s = 0; s < p.steps && !stuck; ++s) {
@@ -151,8 +156,14 @@ __global__ __launch_bounds__(64) void fw_run_kernel(FwRunParams p) {
           stuck = 1;
           break;
         }
-        x = philox((uint32_t)attempts, (uint32_t)(attempts >> 32), (uint32_t)gid,
-                   (uint32_t)(gid >> 32), key0, key1);
+        if (bpos == WAVE) {
+          const uint64_t t = attempts + (uint64_t)lane;
+          pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
+                      in_vgpr(key0), in_vgpr(key1));
+          bpos = 0;
+        }
+        x = U4{rdl(pb.x0, bpos), rdl(pb.x1, bpos), rdl(pb.x2, bpos), rdl(pb.x3, bpos)};
+        ++bpos;
         attempts += 1;
         const uint32_t r = scale64(x.x0, x.x1, (uint32_t)npairs);
         uint32_t j = 0;
