@@ -125,3 +125,43 @@ def test_sharded_handles_merge_bit_identically(gpu_lib):
             lo += c
         keys.append((hc.tobytes(), hb.tobytes(), np.concatenate(sts).tobytes()))
     assert all(kk == keys[0] for kk in keys[1:])
+
+
+def test_c2_time_averaged_histograms_batch_means(gpu_lib):
+    """time-averaged histograms of |cut edges| and |B| (all yields of all
+    chains) from the GPU against independent oracle chains, bin by bin with batch-means
+    error bars (oracle: 16 batches of 16 chains; GPU: 8 handles of 512 chains on disjoint
+    id ranges), plus a chi-square over the populated bins."""
+    n, k, seed, steps = 40, 4, 11, 2000
+    g = grid_graph(n, n)
+    init = block_seed(n, n, 2, 2)
+    bounds = population_bounds(g.total_pop, k, 0.05)
+    thr = metropolis_table(MU, g.maxdeg)
+    E = g.n_edges
+    dg = DeviceGraph(g)
+    gh = {"cut": [], "b": []}
+    for b in range(8):
+        ch = Chains(dg, 512, k, init, proposal="pairs", pop_bounds=bounds, base=MU, seed=seed,
+                    chain_id0=b * 512)
+        ch.run(steps)
+        gh["cut"].append(ch.hist_cut()[:E + 1] / ch.hist_cut().sum())
+        gh["b"].append(ch.hist_b()[:g.n + 1] / ch.hist_b().sum())
+        ch.close()
+    oh = {"cut": [], "b": []}
+    for b in range(16):
+        hc = np.zeros(E + 1 + 64, np.uint64)
+        hb = np.zeros(g.n + 1 + 64, np.uint64)
+        for cid in range((1 << 20) + 16 * b, (1 << 20) + 16 * b + 16):
+            O.run_chain(g, init, k, 1, *bounds, thr, seed, cid, steps, hist_cut=hc, hist_b=hb)
+        oh["cut"].append(hc[:E + 1] / hc.sum())
+        oh["b"].append(hb[:g.n + 1] / hb.sum())
+    for f in ("cut", "b"):
+        G, Q = np.array(gh[f]), np.array(oh[f])
+        pg, po = G.mean(0), Q.mean(0)
+        se = np.sqrt(G.var(0, ddof=1) / len(G) + Q.var(0, ddof=1) / len(Q))
+        live = (po > 0.002) & (se > 0)
+        z = (pg[live] - po[live]) / se[live]
+        assert live.sum() >= 20, f
+        assert np.abs(z).max() < 5.0, (f, np.abs(z).max())
+        chi2 = float((z ** 2).sum())
+        assert sps.chi2.sf(chi2, int(live.sum())) > 1e-3, (f, chi2, int(live.sum()))
