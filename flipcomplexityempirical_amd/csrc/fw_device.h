@@ -494,8 +494,9 @@ struct Ctx {
     uint32_t s = 0;
     const int g0 = lane * PER;
 #pragma unroll
-    for (int t = 0; t < PER; ++t) {
-      gs[t] = (g0 + t < G) ? gsum[g0 + t] : 0u;
+    for (int t = 0; t < PER; ++t) {  // unconditional (clamped) reads, masked values
+      const uint32_t w = gsum[min(g0 + t, G - 1)];
+      gs[t] = g0 + t < G ? w : 0u;
       s += gs[t];
     }
     const uint32_t incl = scan_incl(s);
