@@ -403,6 +403,28 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   const int32_t rule = FULL ? p.accept : FW_ACCEPT_CUT;
   int my_dr, my_dc;
   role_off(q <= 8 ? q : 0, my_dr, my_dc);
+  // 2-bit labels: row-lanes 9..12 also take the cells two steps from v (UU, LL, RR, DD),
+  // so the whole radius-2 diamond is read with one LDS round trip (one cell per lane)
+  // and each 4-neighbour's label set comes from per-label row ballots.  nb_lanes: the
+  // lanes holding the neighbours of this lane's cell other than v.
+  if (LB == 2 && q >= 9 && q <= 12) {
+    my_dr = q == 9 ? -2 : (q == 12 ? 2 : 0);
+    my_dc = q == 10 ? -2 : (q == 11 ? 2 : 0);
+  }
+  const uint32_t nb_lanes = q == 0   ? 0x1Eu
+                            : q == 1 ? (1u << 9) | (1u << 8) | (1u << 5)
+                            : q == 2 ? (1u << 10) | (1u << 8) | (1u << 7)
+                            : q == 3 ? (1u << 11) | (1u << 5) | (1u << 6)
+                            : q == 4 ? (1u << 12) | (1u << 6) | (1u << 7)
+                                     : 0u;
+  // 7x7 window cells of this lane (three per lane, v skipped): offsets from v
+  int win_dr[3], win_dc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int pos = window_pos(q + ROW * t);
+    win_dr[t] = pos / 7 - 3;
+    win_dc[t] = pos % 7 - 3;
+  }
   auto divmod = [&](int x, int& r, int& c) {
     r = (int)__umulhi((uint32_t)x, gm32);
     c = x - r * W;
@@ -616,7 +638,30 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       h.cnt = 0;
       h.has_v = false;
       h.deg = 0;
-      {
+      if constexpr (LB == 2) {
+        // one unconditional read per lane (cells off the grid read v and are masked)
+        const int xr = vr + my_dr, xc = vc + my_dc;
+        const bool inb = (q <= 12) & (xr >= 0) & (xr < H) & (xc >= 0) & (xc < W);
+        const int xx = xr * W + xc;
+        const uint32_t l0 = P::get(lab, inb ? xx : v);
+        h.x = inb ? xx : -1;
+        h.lx = inb ? l0 : NOLAB;
+        const uint32_t m0 = rowbits(ballot(h.lx == 0u), row) & nb_lanes;
+        const uint32_t m1 = rowbits(ballot(h.lx == 1u), row) & nb_lanes;
+        const uint32_t m2 = rowbits(ballot(h.lx == 2u), row) & nb_lanes;
+        const uint32_t m3 = rowbits(ballot(h.lx == 3u), row) & nb_lanes;
+        h.bits = (m0 ? 1u : 0u) | (m1 ? 2u : 0u) | (m2 ? 4u : 0u) | (m3 ? 8u : 0u);
+        if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
+          const uint32_t same = h.lx == 0u ? m0 : h.lx == 1u ? m1 : h.lx == 2u ? m2 : m3;
+          h.cnt = (uint32_t)__popc(m0 | m1 | m2 | m3) - (uint32_t)__popc(same);
+          h.deg = q == 0 ? (int)h.cnt + (int)__popc(same) : 0;
+        }
+        h.has_v = q >= 1 && q <= 4 && inb;
+        if (!(inb && q <= 4)) {
+          h.bits = 0;
+          h.cnt = 0;
+        }
+      } else {
         const int xr = vr + my_dr, xc = vc + my_dc;
         if (q <= 8 && xr >= 0 && xr < H && xc >= 0 && xc < W) {
           h.x = xr * W + xc;
@@ -654,11 +699,16 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         d = row_pick(h.lx, Lc, q);
       } else {
         // distinct foreign labels among the 4 neighbours, then the j-th smallest
-        uint32_t fb = (isnb && h.lx != a) ? (1u << h.lx) : 0u;
-        fb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x111, 0xF, 0xF, true);  // row_shr:1
-        fb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x112, 0xF, 0xF, true);  // row_shr:2
-        fb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x114, 0xF, 0xF, true);  // row_shr:4
-        const uint32_t mask = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x154, 0xF, 0xF, false);  // row_newbcast:4
+        uint32_t mask;
+        if constexpr (LB == 2) {
+          mask = row_first(h.bits) & ~(1u << a);  // row-lane 0 holds v's neighbour label set
+        } else {
+          uint32_t fb = (isnb && h.lx != a) ? (1u << h.lx) : 0u;
+          fb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x111, 0xF, 0xF, true);  // row_shr:1
+          fb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x112, 0xF, 0xF, true);  // row_shr:2
+          fb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x114, 0xF, 0xF, true);  // row_shr:4
+          mask = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x154, 0xF, 0xF, false);  // row_newbcast:4
+        }
         uint32_t mm = mask;
         for (uint32_t t = 0; t < j && t < 15; ++t) mm &= mm - 1;
         d = (uint32_t)(__ffs(mm) - 1);
@@ -685,14 +735,17 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       bool need = go && pop_ok && m >= 2 && !contig;
       if (ballot(need)) {  // 7x7 window flood fill (3 window cells per row-lane)
         uint64_t A = 0;
+        bool inw[3];
+        uint32_t lw[3];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {  // branch-free: clamped read, masked result
-          const int pos = window_pos(q + ROW * t);
-          const int rr = vr - 3 + pos / 7, cw = vc - 3 + pos % 7;
-          const bool inb = rr >= 0 && rr < H && cw >= 0 && cw < W;
-          const uint32_t lw = P::get(lab, inb ? rr * W + cw : v);
-          A |= (uint64_t)rowbits(ballot(inb && lw == a), row) << (ROW * t);
+        for (int t = 0; t < 3; ++t) {  // branch-free: all three reads issued, then masked
+          const int rr = vr + win_dr[t], cw = vc + win_dc[t];
+          inw[t] = (rr >= 0) & (rr < H) & (cw >= 0) & (cw < W);
+          lw[t] = P::get(lab, inw[t] ? rr * W + cw : v);
         }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          A |= (uint64_t)rowbits(ballot(inw[t] & (lw[t] == a)), row) << (ROW * t);
         A = (A & ((1ull << 24) - 1ull)) | ((A >> 24) << 25);
         const int wvd = window_verdict_row(A, q, row, need);
         if (wvd >= 0) {
