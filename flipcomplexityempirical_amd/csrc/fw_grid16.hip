@@ -50,6 +50,7 @@ namespace {
 constexpr int ROW = 16;
 constexpr int MAX_NW = 4;          // waves per workgroup
 constexpr uint32_t SCR_BLOCK = 15;  // scratch code of v during a search
+constexpr int LDS_GUARD = 16;       // bytes in front of the first chain slot
 
 // v's neighbourhood as one lane sees it (labels < 16 here, so 32-bit label sets)
 struct Hood16 {
@@ -100,7 +101,9 @@ __device__ __forceinline__ uint32_t lab_window(const LDS uint8_t* lab, int x) {
   const int bit = (x - 1) * LB;  // x - 1 may be -1: field 0 is then garbage, masked by callers
   const int wi = bit >> 5;       // arithmetic shift: -1 -> -1
   const LDS uint32_t* w = reinterpret_cast<const LDS uint32_t*>(lab);
-  const uint32_t lo0 = w[wi > 0 ? wi : 0];  // unconditional read: no exec-mask branch
+  // wi >= -1: w[-1] is the word before the slot (the previous slot's tail, or the 16-B
+  // guard in front of slot 0), masked below; one base address -> one ds_read2_b32
+  const uint32_t lo0 = w[wi];
   const uint32_t lo = wi >= 0 ? lo0 : 0u;
   const uint32_t hi = w[wi + 1];
   const uint64_t both = ((uint64_t)hi << 32) | lo;
@@ -161,10 +164,12 @@ __device__ __forceinline__ uint32_t onehot4(uint32_t s) {  // bytes 0..3 -> 1 <<
   return __builtin_amdgcn_perm(0u, 0x08040201u, s);
 }
 __device__ __forceinline__ uint32_t low_bytes(int t) {  // 0xFF in bytes 0..t-1
-  return t >= 4 ? 0xFFFFFFFFu : (t <= 0 ? 0u : (1u << (8 * t)) - 1u);
+  // branch-free: clamp, then a select (no exec-mask branch in the level-2 walk)
+  const uint32_t tc = (uint32_t)min(max(t, 0), 4);
+  return tc == 4u ? 0xFFFFFFFFu : (1u << (8u * tc)) - 1u;
 }
 __device__ __forceinline__ uint32_t byte_clear(int t) {  // all bytes but byte t (t in 0..3)
-  return t >= 0 && t < 4 ? ~(0xFFu << (8 * t)) : 0xFFFFFFFFu;
+  return (uint32_t)t < 4u ? ~(0xFFu << (8 * t)) : 0xFFFFFFFFu;
 }
 // per byte: 0x80 where the one-hot bytes a and b differ (different labels)
 __device__ __forceinline__ uint32_t ne_bytes(uint32_t a, uint32_t b) {
@@ -198,9 +203,10 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
   const int c0 = x0 - r0 * W;
   const int tw = W - c0;  // first byte on the next grid row (>= 4: none)
   const uint32_t mN = low_bytes(n - x0);
-  const uint32_t mU = r0 == 0 ? ~low_bytes(tw) : 0xFFFFFFFFu;
-  const uint32_t mD = r0 == H - 1 ? low_bytes(tw) ^ 0xFFFFFFFFu
-                                  : (r0 + 1 == H - 1 ? low_bytes(tw) : 0xFFFFFFFFu);
+  const uint32_t lowtw = low_bytes(tw);
+  const uint32_t mU = r0 == 0 ? ~lowtw : 0xFFFFFFFFu;
+  uint32_t mD = r0 == H - 1 ? ~lowtw : 0xFFFFFFFFu;
+  mD = r0 + 1 == H - 1 ? lowtw : mD;
   const uint32_t mL = byte_clear(c0 == 0 ? 0 : tw);
   const uint32_t mR = byte_clear(tw - 1);
   if constexpr (MODE != FW_PROPOSE_CUTEDGE) {
@@ -387,7 +393,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   const int D = (int)in_vgpr((uint32_t)p.g.maxdeg), G = (int)in_vgpr((uint32_t)p.G);
   const int k = (int)in_vgpr((uint32_t)p.k);
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
-  LDS uint8_t* const lab = sm + (wv * 4 + row) * p.slot_stride;  // this row's chain slot
+  // this row's chain slot (after a 16-B guard: lab_window may read the word before a slot)
+  LDS uint8_t* const lab = sm + LDS_GUARD + (wv * 4 + row) * p.slot_stride;
   LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);  // u16 pairs
   LDS uint8_t* const scr = sm + p.off_scr;                                        // shared
   LDS uint32_t* const list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list16);  // shared
@@ -710,7 +717,12 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           mask = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fb, 0x154, 0xF, 0xF, false);  // row_newbcast:4
         }
         uint32_t mm = mask;
-        for (uint32_t t = 0; t < j && t < 15; ++t) mm &= mm - 1;
+        if constexpr (LB == 2) {  // k <= 4: at most 3 foreign labels, j <= 2 (no loop)
+          const uint32_t m1 = mm & (mm - 1u), m2 = m1 & (m1 - 1u);
+          mm = j == 0u ? mm : (j == 1u ? m1 : m2);
+        } else {
+          for (uint32_t t = 0; t < j && t < 15; ++t) mm &= mm - 1;
+        }
         d = (uint32_t)(__ffs(mm) - 1);
       }
       const uint32_t amb = rowbits(ballot(isnb && h.lx == a), row) >> 1;
@@ -720,8 +732,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 
       // ---- population bound (lane q holds district q)
       const int32_t pv = unit_pop ? 1 : (int32_t)p.g.pop[v];
-      const bool bad = ((uint32_t)q == a && pops - pv < pop_lo) ||
-                       ((uint32_t)q == d && pops + pv > pop_hi);
+      const bool bad = (((uint32_t)q == a) & (pops - pv < pop_lo)) |
+                       (((uint32_t)q == d) & (pops + pv > pop_hi));
       const bool pop_ok = rowbits(ballot(bad), row) == 0u;
 
       STAMP(3);  // gather, target, Δcut, population
@@ -731,8 +743,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const int NE = (rbits8 >> 4) & 1, SE = (rbits8 >> 5) & 1, SW = (rbits8 >> 6) & 1,
                 NW = (rbits8 >> 7) & 1;
       const int lNE = pN & pE & NE, lES = pE & pS & SE, lSW = pS & pW & SW, lWN = pW & pN & NW;
-      bool contig = m == 1 || (m >= 2 && m - (lNE + lES + lSW + lWN) <= 1);
-      bool need = go && pop_ok && m >= 2 && !contig;
+      // bitwise, not short-circuit: no exec-mask branches
+      bool contig = (m == 1) | ((m >= 2) & (m - (lNE + lES + lSW + lWN) <= 1));
+      bool need = go & pop_ok & (m >= 2) & !contig;
       if (ballot(need)) {  // 7x7 window flood fill (3 window cells per row-lane)
         uint64_t A = 0;
         bool inw[3];
@@ -796,7 +809,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (lk & 4) merge(sx(3), sx(1));  // S-W
         if (lk & 8) merge(sx(1), sx(0));  // W-N
         uint64_t bn = 0, bd = 0;
-        const bool ok = grid_race<LB>(sm + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
+        const bool ok = grid_race<LB>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
                                       p.qcap16, W, H, p.g.gm32, lane, vv, aa, mr, srcn, cls, bn,
                                       bd);
         if (row == rr) {
@@ -1011,7 +1024,7 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
   int best_nw = 0, best_chains = 0, best_lds = 0;
   for (int nw = 1; nw <= MAX_NW; ++nw) {
-    const int lds = 4 * nw * stride + p.scr_bytes + 4 * p.qcap16;
+    const int lds = LDS_GUARD + 4 * nw * stride + p.scr_bytes + 4 * p.qcap16;
     if (lds > 160 * 1024 - 256) break;
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
       return -1;
@@ -1027,7 +1040,7 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   }
   if (best_nw == 0) return -1;
   p.nw = best_nw;
-  p.off_scr = 4 * best_nw * stride;
+  p.off_scr = LDS_GUARD + 4 * best_nw * stride;
   p.off_list16 = p.off_scr + p.scr_bytes;
   p.lds16 = best_lds;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, best_lds) != hipSuccess)
