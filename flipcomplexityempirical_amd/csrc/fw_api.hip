@@ -72,11 +72,30 @@ int list_cap(int dflt) {
   return v >= 1 ? v : dflt;
 }
 
+// x / gw == (x * m) >> s for every x < 2^15 with m < 2^17 (so the grid kernel divides with
+// one full-rate 24-bit multiply), verified exhaustively; m = 0 if no shift works
+void grid_div24(int gw, uint32_t* m_out, uint32_t* s_out) {
+  *m_out = 0;
+  *s_out = 0;
+  for (uint32_t sh = 0; gw > 0 && sh < 32; ++sh) {
+    const uint64_t m = (((uint64_t)1 << sh) + (uint64_t)gw - 1) / (uint64_t)gw;
+    if (m >= ((uint64_t)1 << 17)) break;
+    bool ok = m > 0;
+    for (uint64_t x = 0; x < ((uint64_t)1 << 15) && ok; ++x) ok = ((x * m) >> sh) == x / (uint64_t)gw;
+    if (ok) {
+      *m_out = (uint32_t)m;
+      *s_out = sh;
+      return;
+    }
+  }
+}
+
 }  // namespace
 
 struct fw_graph {
   int device = 0;
   int32_t n = 0, nnz = 0, maxdeg = 0, gw = 0, gh = 0;
+  uint32_t gm24 = 0, gs24 = 0;  // grid_div24
   std::vector<int32_t> rowptr, col;
   std::vector<int64_t> pop;  // empty: unit populations
   int32_t* d_rowptr = nullptr;
@@ -104,6 +123,8 @@ struct fw_graph {
     // exact x / gw for x < 2^21 (the grid path is only taken for n < 2^21)
     g.gmagic = gw ? (((uint64_t)1 << 42) + (uint64_t)gw - 1) / (uint64_t)gw : 0;
     g.gm32 = gw ? (uint32_t)((((uint64_t)1 << 32) + (uint64_t)gw - 1) / (uint64_t)gw) : 0;
+    g.gm24 = gm24;
+    g.gs24 = gs24;
     return g;
   }
 };
@@ -274,6 +295,7 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   }
   g->gw = n < (1 << 21) ? detect_grid(g->rowptr, g->col, n) : 0;
   g->gh = g->gw ? n / g->gw : 0;
+  grid_div24(g->gw, &g->gm24, &g->gs24);
   if (hipSetDevice(device) != hipSuccess) {
     delete g;
     return fail(FW_EHIP, "hipSetDevice(%d) failed", device);
@@ -417,7 +439,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   const char* no16 = getenv("FLIPWALK_NO_GRID16");
   int64_t total_pop = 0;
   for (int x = 0; x < n; ++x) total_pop += g->popof(x);
-  const bool use16 = fw_grid16_candidate(g->gw, D, G, k, total_pop) && !(no16 && no16[0] == '1');
+  const bool use16 = fw_grid16_candidate(g->gw, D, G, k, total_pop) && g->gm24 != 0 &&
+                     !(no16 && no16[0] == '1');
   const int lb = use16 ? (k <= 4 ? 2 : 4) : pick_lb(k, g->maxdeg);
   if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 

@@ -62,6 +62,17 @@ struct Hood16 {
   int deg;        // degree of x
 };
 
+// x / W for 0 <= x < 2^15 with a full-rate 24-bit multiply (host-verified magic)
+struct GDiv {
+  uint32_t m, s;
+  __device__ __forceinline__ int operator()(int x) const {
+    return (int)(__umul24((uint32_t)x, m) >> s);
+  }
+};
+// r * W (+ c): full-rate 24-bit multiply (grid coordinates < 2^14; out-of-grid values
+// are computed but never used)
+__device__ __forceinline__ int mulW(int r, int W) { return (int)__umul24((uint32_t)r, (uint32_t)W); }
+
 __device__ __forceinline__ uint32_t rowbits(uint64_t bal, int row) {
   return (uint32_t)(bal >> (row * ROW)) & 0xFFFFu;
 }
@@ -116,7 +127,7 @@ __device__ __forceinline__ uint32_t lab_window(const LDS uint8_t* lab, int x) {
 // four nodes has that neighbour; per-node row/column checks mask the rest.
 template <int LB, int MODE>
 __device__ __forceinline__ void weights4(const LDS uint8_t* lab, int x0, int W, int H, int n,
-                                         uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
+                                         GDiv gd, uint32_t& w4, uint32_t& cd4) {
   constexpr uint32_t M = (1u << LB) - 1u;
   w4 = 0;
   cd4 = 0;
@@ -124,8 +135,8 @@ __device__ __forceinline__ void weights4(const LDS uint8_t* lab, int x0, int W, 
   const uint32_t own = lab_window<LB>(lab, x0);
   const uint32_t up = x0 + 3 - W >= 0 ? lab_window<LB>(lab, x0 - W) : 0u;
   const uint32_t dn = x0 + W < n ? lab_window<LB>(lab, x0 + W) : 0u;
-  const int r0 = (int)__umulhi((uint32_t)x0, gm32);
-  const int c0 = x0 - r0 * W;
+  const int r0 = gd(x0);
+  const int c0 = x0 - mulW(r0, W);
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
     int ct = c0 + tt, rt = r0;
@@ -182,7 +193,7 @@ __device__ __forceinline__ uint32_t byte_popc(uint32_t f) {  // per-byte popcoun
 
 template <int MODE, bool NEED_CD>
 __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, int W, int H, int n,
-                                              uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
+                                              GDiv gd, uint32_t& w4, uint32_t& cd4) {
   w4 = 0;
   cd4 = 0;
   // branch-free: every read is issued at a valid position and its result masked (mN is
@@ -199,8 +210,8 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
   const uint32_t R = __builtin_amdgcn_alignbyte(o_hi, o_lo, 2);  // x+1
   const uint32_t U = onehot4(spread4(up >> 2)), Dn = onehot4(spread4(dn >> 2));
   // which of the four nodes have each neighbour (W >= 4: at most one row wrap, at tw)
-  const int r0 = (int)__umulhi((uint32_t)x0, gm32);
-  const int c0 = x0 - r0 * W;
+  const int r0 = gd(x0);
+  const int c0 = x0 - mulW(r0, W);
   const int tw = W - c0;  // first byte on the next grid row (>= 4: none)
   const uint32_t mN = low_bytes(n - x0);
   const uint32_t lowtw = low_bytes(tw);
@@ -224,11 +235,11 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
 // weights (and, when NEED_CD, cut degrees) of nodes x0..x0+3, one per byte
 template <int LB, int MODE, bool NEED_CD>
 __device__ __forceinline__ void weights4x(const LDS uint8_t* lab, int x0, int W, int H, int n,
-                                          uint32_t gm32, uint32_t& w4, uint32_t& cd4) {
+                                          GDiv gd, uint32_t& w4, uint32_t& cd4) {
   if constexpr (LB == 2)
-    weights4_swar<MODE, NEED_CD>(lab, x0, W, H, n, gm32, w4, cd4);
+    weights4_swar<MODE, NEED_CD>(lab, x0, W, H, n, gd, w4, cd4);
   else
-    weights4<LB, MODE>(lab, x0, W, H, n, gm32, w4, cd4);
+    weights4<LB, MODE>(lab, x0, W, H, n, gd, w4, cd4);
 }
 
 // bytes of w (each < 64) summed
@@ -270,7 +281,7 @@ __device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
 // Wave-cooperative: all 64 lanes call it for one chain; the caller holds the lock.
 template <int LB>
 __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t* list,
-                          GLB uint32_t* spill, int qcap, int W, int H, uint32_t gm32, int lane,
+                          GLB uint32_t* spill, int qcap, int W, int H, GDiv gd, int lane,
                           int v, uint32_t a, int m, int src, uint64_t cls, uint64_t& bfs_nodes,
                           uint64_t& bfs_deg) {
   using P = PK<LB>;
@@ -306,8 +317,8 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
       const bool act = idx < le;
       const int x = act ? (int)list_get(idx) : 0;
       const uint32_t o = act ? S::get(scr, x) - 1u : 0u;
-      const int xr = (int)__umulhi((uint32_t)x, gm32);
-      const int xc = x - xr * W;
+      const int xr = gd(x);
+      const int xc = x - mulW(xr, W);
       if (act) my_deg += (uint32_t)((xr > 0) + (xc > 0) + (xc < W - 1) + (xr < H - 1));
       bfs_nodes += (uint64_t)__popcll(ballot(act));
 #pragma unroll
@@ -406,7 +417,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   // the one-chain-per-wave kernel); clamped so comparisons keep their meaning
   const int32_t pop_lo = (int32_t)in_vgpr((uint32_t)(int32_t)max(p.pop_lo, (int64_t)INT32_MIN));
   const int32_t pop_hi = (int32_t)in_vgpr((uint32_t)(int32_t)min(p.pop_hi, (int64_t)INT32_MAX));
-  const uint32_t gm32 = in_vgpr(p.g.gm32);
+  const GDiv gd{in_vgpr(p.g.gm24), in_vgpr(p.g.gs24)};
   const int32_t rule = FULL ? p.accept : FW_ACCEPT_CUT;
   int my_dr, my_dc;
   role_off(q <= 8 ? q : 0, my_dr, my_dc);
@@ -433,8 +444,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     win_dc[t] = pos % 7 - 3;
   }
   auto divmod = [&](int x, int& r, int& c) {
-    r = (int)__umulhi((uint32_t)x, gm32);
-    c = x - r * W;
+    r = gd(x);
+    c = x - mulW(r, W);
   };
   STAMP_DECL
 
@@ -499,7 +510,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           uint32_t w4, cd4;
-          weights4x<LB, MODE, true>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, p.g.gm32, w4, cd4);
+          weights4x<LB, MODE, true>(lab, (2 * t2 + h) * 64 + q * 4, W, H, n, gd, w4, cd4);
           const uint32_t ws = bsum4m(w4);
           cut2 += bsum4m(cd4);
           bn += ((cd4 & 0xFFu) != 0) + ((cd4 & 0xFF00u) != 0) + ((cd4 & 0xFF0000u) != 0) +
@@ -615,15 +626,17 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
-      weights4x<LB, MODE, false>(lab, x0, W, H, n, gm32, w4, cd4);
-      const uint32_t pref = w4 * 0x01010101u;  // byte t: weights of nodes 0..t (<= 16)
+      weights4x<LB, MODE, false>(lab, x0, W, H, n, gd, w4, cd4);
+      // byte t: weights of nodes 0..t (<= 16); two shift-adds, not a quarter-rate multiply
+      const uint32_t pref1 = w4 + (w4 << 8);
+      const uint32_t pref = pref1 + (pref1 << 16);
       const uint32_t ws = pref >> 24;
       const uint32_t incl2 = row_scan(ws);
       const uint32_t rb2 = rowbits(ballot(incl2 > r1), row);
       const int L2 = __ffs(rb2) - 1;
       const uint32_t r2 = min(r1 - (incl2 - ws), 127u);  // < ws on the chosen lane
       // first byte with prefix > r2 (SWAR compare; no borrow across bytes as r2 < 128)
-      const uint32_t gt = ((pref | 0x80808080u) - (r2 + 1u) * 0x01010101u) & 0x80808080u;
+      const uint32_t gt = ((pref | 0x80808080u) - __builtin_amdgcn_perm(0u, r2 + 1u, 0u)) & 0x80808080u;
       const int t2 = gt ? (__ffs(gt) - 1) >> 3 : 3;
       const uint32_t bef2 = t2 ? (pref >> (8 * t2 - 8)) & 0xFFu : 0u;
       const uint32_t pk2 = row_pick(((uint32_t)(q * 4 + t2) << 16) | ((r2 - bef2) & 0xFFFFu), L2, q);
@@ -649,7 +662,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         // one unconditional read per lane (cells off the grid read v and are masked)
         const int xr = vr + my_dr, xc = vc + my_dc;
         const bool inb = (q <= 12) & (xr >= 0) & (xr < H) & (xc >= 0) & (xc < W);
-        const int xx = xr * W + xc;
+        const int xx = mulW(xr, W) + xc;
         const uint32_t l0 = P::get(lab, inb ? xx : v);
         h.x = inb ? xx : -1;
         h.lx = inb ? l0 : NOLAB;
@@ -754,7 +767,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         for (int t = 0; t < 3; ++t) {  // branch-free: all three reads issued, then masked
           const int rr = vr + win_dr[t], cw = vc + win_dc[t];
           inw[t] = (rr >= 0) & (rr < H) & (cw >= 0) & (cw < W);
-          lw[t] = P::get(lab, inw[t] ? rr * W + cw : v);
+          lw[t] = P::get(lab, inw[t] ? mulW(rr, W) + cw : v);
         }
 #pragma unroll
         for (int t = 0; t < 3; ++t)
@@ -810,7 +823,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (lk & 8) merge(sx(1), sx(0));  // W-N
         uint64_t bn = 0, bd = 0;
         const bool ok = grid_race<LB>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
-                                      p.qcap16, W, H, p.g.gm32, lane, vv, aa, mr, srcn, cls, bn,
+                                      p.qcap16, W, H, gd, lane, vv, aa, mr, srcn, cls, bn,
                                       bd);
         if (row == rr) {
           contig = ok;

@@ -23,6 +23,7 @@ struct FwGraphDev {
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)
   uint64_t gmagic;        // ceil(2^42 / gw): x / gw == (x * gmagic) >> 42 for x < 2^21
   uint32_t gm32;          // ceil(2^32 / gw): x / gw == mulhi(x, gm32) for x * gw < 2^32
+  uint32_t gm24, gs24;    // x / gw == umul24(x, gm24) >> gs24 for x < 2^15 (0: none found)
 };
 
 struct FwRunParams {
