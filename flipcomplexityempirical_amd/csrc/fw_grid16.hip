@@ -846,25 +846,25 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       }
       // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
       uint32_t wo = 0, wn = 0;
-      const bool mine = q <= 4 && h.x >= 0;
-      if (mine) {
-        if (q == 0) {
-          if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
-            wo = (uint32_t)(h.deg - m);
-            wn = (uint32_t)(h.deg - nbd);
-          } else {
-            wo = (uint32_t)__popc(h.bits & ~(1u << a));
-            wn = (uint32_t)__popc(h.bits & ~(1u << d));
-          }
-        } else if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
-          wo = h.cnt + (h.has_v && a != h.lx);
-          wn = h.cnt + (h.has_v && d != h.lx);
-        } else {
-          const uint32_t keep = ~(1u << h.lx);
-          wo = (uint32_t)__popc((h.bits | (h.has_v ? 1u << a : 0u)) & keep);
-          wn = (uint32_t)__popc((h.bits | (h.has_v ? 1u << d : 0u)) & keep);
-        }
+      const bool mine = (q <= 4) & (h.x >= 0);
+      // branch-free (selects, no exec-mask if/else between v's lane and its neighbours')
+      if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
+        const uint32_t wo_v = (uint32_t)(h.deg - m), wn_v = (uint32_t)(h.deg - nbd);
+        const uint32_t wo_u = h.cnt + (uint32_t)(h.has_v & (a != h.lx));
+        const uint32_t wn_u = h.cnt + (uint32_t)(h.has_v & (d != h.lx));
+        wo = q == 0 ? wo_v : wo_u;
+        wn = q == 0 ? wn_v : wn_u;
+      } else {
+        // v: its neighbour label set minus the old / new label; a neighbour u: its set
+        // (plus v's old / new label) minus u's own label
+        const uint32_t hv = h.has_v ? 0xFFFFFFFFu : 0u;
+        const uint32_t ka = q == 0 ? ~(1u << a) : ~(1u << h.lx);
+        const uint32_t kd = q == 0 ? ~(1u << d) : ~(1u << h.lx);
+        wo = (uint32_t)__popc((h.bits | ((1u << a) & hv)) & ka);
+        wn = (uint32_t)__popc((h.bits | ((1u << d) & hv)) & kd);
       }
+      wo = mine ? wo : 0u;
+      wn = mine ? wn : 0u;
       const uint64_t b_plus = ballot(valid && mine && wo == 0 && wn > 0);
       const uint64_t b_minus = ballot(valid && mine && wo > 0 && wn == 0);
       const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
@@ -884,9 +884,9 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         } else {  // integer form of u53(x2, x3) < thr_l (exact)
           acc_l = (((uint64_t)(x.x2 >> 5) << 26) | (uint64_t)(x.x3 >> 6)) < thr53_l;
         }
-        accepted = valid && ((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u);
+        accepted = valid & (((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u) != 0u);
       }
-      if (valid && p.trace && q == 0)
+      if (p.trace != nullptr && valid && q == 0)
         p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
       n_steps += valid ? 1u : 0u;
       if (maps_on && accepted) {  // spatial observables: fire-and-forget atomics
@@ -911,7 +911,12 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           lds_add(gsum + (h.x >> 7), (wn - wo) << (16 * ((h.x >> 6) & 1)));
       }
       lds_order();
-      const int dnp = (int)row_sum(accepted && mine ? wn - wo : 0u);
+      // lanes 0..4 hold the changes: a 3-step row_shr scan leaves their sum on lane 4
+      uint32_t dl = accepted && mine ? wn - wo : 0u;
+      dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x111, 0xF, 0xF, true);
+      dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x112, 0xF, 0xF, true);
+      dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x114, 0xF, 0xF, true);
+      const int dnp = (int)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x154, 0xF, 0xF, false);  // row_newbcast:4
       if (accepted) {
         n_acc += 1;
         if (FULL && p.sched) sched_row(n_acc);
