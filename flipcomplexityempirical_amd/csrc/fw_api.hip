@@ -456,6 +456,10 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   FwRunParams& p = c->p;
   p.qcap = list_cap(256);
   p.qcap16 = list_cap(384);
+  {  // FLIPWALK_NO_BITBOARD=1: the grid kernel runs every exact search as the list search
+    const char* e = getenv("FLIPWALK_NO_BITBOARD");
+    p.no_bb = e && e[0] == '1' ? 1 : 0;
+  }
   // +8: the grid kernels read label dwords one past the last node
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
   p.off_gsum = p.lab_bytes;

@@ -25,8 +25,8 @@
 
 #ifdef FW_STAMPS
 // Diagnostic build only (libflipwalk_stamps.so): per-phase s_memtime shares.
-__device__ unsigned long long g_stamps[8];
-#define STAMP_DECL uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_t0 = 0;
+__device__ unsigned long long g_stamps[16];
+#define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_t0 = 0;
 #define STAMP(i)                                              \
   do {                                                        \
     __builtin_amdgcn_sched_barrier(0);                        \
@@ -38,8 +38,10 @@ __device__ unsigned long long g_stamps[8];
   } while (0)
 #define STAMP_FLUSH                                           \
   if (__lane_id() == 0)                                       \
-    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stamps[i_], (unsigned long long)st_acc[i_]);
+    for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_stamps[i_], (unsigned long long)st_acc[i_]);
+#define STAMP_COUNT(i, v) st_acc[i] += (uint64_t)(v)
 #else
+#define STAMP_COUNT(i, v)
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_FLUSH
@@ -251,7 +253,12 @@ __device__ __forceinline__ uint32_t bsum4m(uint32_t v) { return (v * 0x01010101u
 // of sources in one window component are equal and other fills disjoint, so the
 // sequential verdict is order-free: 1 if some fill holds every source, else 0 if some
 // fill touches no border, else -1 (undecided).  Row-uniform result.
-__device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bool need) {
+__device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bool need, uint32_t& nflood) {
+#ifdef FW_STAMPS
+#define FLOOD_COUNT ++nflood
+#else
+#define FLOOD_COUNT
+#endif
   const uint64_t C0 = 0x0040810204081ull, C6 = C0 << 6;
   const uint64_t BORDER = C0 | C6 | 0x7Full | (0x7Full << 42);
   const uint64_t src = A & ((1ull << 17) | (1ull << 23) | (1ull << 25) | (1ull << 31));
@@ -262,6 +269,7 @@ __device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bo
       const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
       if (y == x) break;
       x = y;
+      FLOOD_COUNT;
     }
   }
   const uint32_t full = rowbits(ballot(x != 0ull && (x & src) == src), row);
@@ -385,6 +393,145 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
   if (lane == 0) scr_clear(scr, v);
   lds_order();
   return verdict == 1;
+}
+
+// the value of the previous / next lane (wave_shr:1 / wave_shl:1 DPP; 0 at the wave's ends)
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, true);
+}
+// cells of X and their 4-neighbours (lane = grid row, bit = column)
+__device__ __forceinline__ uint32_t dilate32(uint32_t x) {
+  return x | (x << 1) | (x >> 1) | from_prev_lane(x) | from_next_lane(x);
+}
+
+// grid_race on bitboards (2-bit labels): a 64-row x 32-column window around v, lane i =
+// grid row vr - 32 + i, bit b = column vc - 16 + b, one u32 of a-labelled cells (v
+// excluded) per lane.  Level by level it holds the sets the list search builds: per
+// source direction d (0 up, 1 left, 2 right, 3 down) the frontier cells reached from d,
+// and the cells new at the next level.  Two classes merge when a frontier cell of one is
+// adjacent to a frontier cell or to a new cell of the other: exactly the merges the list
+// search makes, whatever its claim order.  The stopping rules are the list search's, so
+// the verdict and the counters (cells of the processed levels, their degrees) equal its
+// own and the oracle's contiguous_after.  No scratch, no lock, one VGPR per set.
+// Returns -1 (nothing counted) when a frontier about to be processed holds a window-edge
+// cell whose outward neighbour is on the grid: the caller then runs grid_race.
+__device__ int grid_race_bb(const LDS uint8_t* lab, int W, int H, int lane, int vr, int vc,
+                            uint32_t a, uint32_t am4, uint32_t lk, uint64_t& bfs_nodes,
+                            uint64_t& bfs_deg) {
+  const int r = vr - 32 + lane, c0 = vc - 16;
+  const bool rin = (r >= 0) & (r < H);
+  // 64 label bits from column c0 of row r (c0 >= -16: at most 4 B in front of the row,
+  // i.e. the 16-B guard or the previous slot; past the end the group sums; all masked)
+  const int bit = (mulW(rin ? r : vr, W) + c0) * 2;
+  const LDS uint32_t* wp = reinterpret_cast<const LDS uint32_t*>(lab) + (bit >> 5);
+  const uint32_t sh = (uint32_t)bit & 31u;
+  const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+  const uint32_t pat = a * 0x55555555u;
+  auto eq16 = [&](uint32_t d) {  // 16 labels -> 16 bits "label == a"
+    const uint32_t x = d ^ pat;
+    uint32_t e = ~(x | (x >> 1)) & 0x55555555u;
+    e = (e | (e >> 1)) & 0x33333333u;
+    e = (e | (e >> 2)) & 0x0F0F0F0Fu;
+    e = (e | (e >> 4)) & 0x00FF00FFu;
+    return (e | (e >> 8)) & 0x0000FFFFu;
+  };
+  uint32_t A = eq16(__builtin_amdgcn_alignbit(w1, w0, sh)) |
+               (eq16(__builtin_amdgcn_alignbit(w2, w1, sh)) << 16);
+  const int lo_cut = c0 < 0 ? -c0 : 0;  // bits of columns < 0
+  const int hi_n = W - c0;              // bits >= hi_n: columns >= W (hi_n >= 17)
+  uint32_t cm = ~0u << lo_cut;
+  if (hi_n < 32) cm &= (1u << hi_n) - 1u;
+  A &= rin ? cm : 0u;
+  if (lane == 32) A &= ~(1u << 16);  // v
+  // window-edge cells with an on-grid neighbour outside the window
+  uint32_t E = ((lane == 0) & (r > 0)) | ((lane == 63) & (r < H - 1)) ? ~0u : 0u;
+  if (c0 > 0) E |= 1u;
+  if (c0 + 31 < W - 1) E |= 1u << 31;
+  E &= A;
+  // frontier per direction; sources up (31, 16), left (32, 15), right (32, 17), down (33, 16)
+  uint32_t F[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int sl = d == 0 ? 31 : (d == 3 ? 33 : 32), sb = d == 1 ? 15 : (d == 2 ? 17 : 16);
+    F[d] = (lane == sl && ((am4 >> d) & 1u)) ? (1u << sb) : 0u;
+  }
+  // class of direction d: 4-bit member mask at bits 4d (uniform)
+  uint32_t M = 0x8421u;
+  auto unite = [&](int i, int j) {
+    const uint32_t m = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if ((m >> d) & 1u) M = (M & ~(15u << (4 * d))) | (m << (4 * d));
+  };
+  if (lk & 1u) unite(0, 2);  // N-E
+  if (lk & 2u) unite(2, 3);  // E-S
+  if (lk & 4u) unite(3, 1);  // S-W
+  if (lk & 8u) unite(1, 0);  // W-N
+  auto n_classes = [&]() {
+    int nc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      nc += (int)(((am4 >> d) & 1u) && (__ffs((M >> (4 * d)) & 15u) - 1) == d);
+    return nc;
+  };
+  uint32_t V = F[0] | F[1] | F[2] | F[3];
+  int verdict = -1;
+  uint32_t P;  // processed cells
+  for (;;) {
+    const uint32_t lvl = F[0] | F[1] | F[2] | F[3];
+    if (n_classes() == 1) {
+      verdict = 1;
+      P = V & ~lvl;
+      break;
+    }
+    if (ballot((lvl & E) != 0u)) return -1;
+    uint32_t D[4], nw = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      D[d] = ((am4 >> d) & 1u) ? dilate32(F[d]) & A : 0u;
+      nw |= D[d];
+    }
+    nw &= ~V;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 4; ++j) {
+        if (!((am4 >> i) & 1u) || !((am4 >> j) & 1u) || ((M >> (4 * i + j)) & 1u)) continue;
+        if (ballot((D[i] & (F[j] | (D[j] & nw))) != 0u)) unite(i, j);
+      }
+    uint32_t reach = 0;  // directions with a new cell
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      F[d] = D[d] & nw;
+      reach |= ballot(F[d] != 0u) ? (1u << d) : 0u;
+    }
+    P = V;
+    if (n_classes() == 1) {
+      verdict = 1;
+      break;
+    }
+    // a class none of whose directions reached a new cell is closed: disconnected
+    bool closed = false;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      closed |= ((am4 >> d) & 1u) && (reach & (M >> (4 * d)) & 15u) == 0u;
+    if (closed) {
+      verdict = 0;
+      break;
+    }
+    V |= nw;
+  }
+  // counters over the processed cells: degree = on-grid 4-neighbours
+  const uint32_t pc = (uint32_t)__popc(P);
+  uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
+  if (c0 <= 0) dg -= (P >> (-c0)) & 1u;                // column 0
+  if (hi_n <= 32) dg -= (P >> (hi_n - 1)) & 1u;        // column W - 1
+  bfs_nodes += wave_sum(pc);
+  bfs_deg += wave_sum(dg);
+  return verdict;
 }
 
 // FULL = false: the lean instantiation for the common configuration (cut_accept, no
@@ -773,33 +920,54 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         for (int t = 0; t < 3; ++t)
           A |= (uint64_t)rowbits(ballot(inw[t] & (lw[t] == a)), row) << (ROW * t);
         A = (A & ((1ull << 24) - 1ull)) | ((A >> 24) << 25);
-        const int wvd = window_verdict_row(A, q, row, need);
+        uint32_t nflood = 0;
+        const int wvd = window_verdict_row(A, q, row, need, nflood);
+        STAMP_COUNT(12, 1);
+        STAMP_COUNT(13, __builtin_amdgcn_readfirstlane(__reduce_max_sync(~0ull, nflood)));
         if (wvd >= 0) {
           contig = wvd == 1;
           need = false;
         }
       }
+      STAMP(7);  // ring + 7x7 window
       uint64_t rows_need = ballot(q == 0 && need);
-      if (rows_need) {
-        // the scratch and visit list are shared by the workgroup's waves
-        if (lane == 0) {
-          int expect = 0;
-          while (!__hip_atomic_compare_exchange_strong(&s_lock, &expect, 1, __ATOMIC_ACQUIRE,
-                                                       __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            expect = 0;
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        lds_order();
-      }
+      bool locked = false;
       while (rows_need) {  // wave-cooperative exact search, one chain slot at a time
         const int L0 = __ffsll((unsigned long long)rows_need) - 1;
         rows_need &= rows_need - 1;
         const int rr = L0 >> 4;
-        const int vv = rdl(v, L0);
         const uint32_t aa = rdl(a, L0);
         const uint32_t am4 = rdl(amb, L0);
+        const uint32_t lk = rdl((uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)), L0);
+        uint64_t bn = 0, bd = 0;
+        int verdict = -1;
+        if (LB == 2 && !p.no_bb)  // bitboard form first; the list search past its window
+          verdict = grid_race_bb(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, W, H, lane,
+                                 rdl(vr, L0), rdl(vc, L0), aa, am4, lk, bn, bd);
+        if (verdict >= 0) {
+          if (row == rr) {
+            contig = verdict == 1;
+            n_bfs += 1;
+            n_bfsn += bn;
+            n_bfsd += bd;
+          }
+          continue;
+        }
+        if (!locked) {
+          // the scratch and visit list are shared by the workgroup's waves
+          if (lane == 0) {
+            int expect = 0;
+            while (!__hip_atomic_compare_exchange_strong(&s_lock, &expect, 1, __ATOMIC_ACQUIRE,
+                                                         __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              expect = 0;
+              __builtin_amdgcn_s_sleep(1);
+            }
+          }
+          lds_order();
+          locked = true;
+        }
+        const int vv = rdl(v, L0);
         const int mr = __popc(am4);
         // sources in CSR order (up, left, right, down) into lanes 0..m-1
         int srcn = -1;
@@ -811,7 +979,6 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           if (lane == i) srcn = val;
         }
         uint64_t cls = lane < mr ? (1ull << lane) : 0ull;
-        const uint32_t lk = rdl((uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)), L0);
         auto sx = [&](int b) { return __popc(am4 & ((1u << b) - 1u)); };
         auto merge = [&](int s1, int s2) {
           const uint64_t nm = rdl64(cls, s1) | rdl64(cls, s2);
@@ -821,7 +988,6 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (lk & 2) merge(sx(2), sx(3));  // E-S
         if (lk & 4) merge(sx(3), sx(1));  // S-W
         if (lk & 8) merge(sx(1), sx(0));  // W-N
-        uint64_t bn = 0, bd = 0;
         const bool ok = grid_race<LB>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
                                       p.qcap16, W, H, gd, lane, vv, aa, mr, srcn, cls, bn,
                                       bd);
@@ -831,11 +997,11 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           n_bfsn += bn;
           n_bfsd += bd;
         }
-        if (rows_need == 0 && lane == 0)
-          __hip_atomic_store(&s_lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      if (locked && lane == 0)
+        __hip_atomic_store(&s_lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 
-      STAMP(4);  // ring test + exact searches
+      STAMP(4);  // exact searches
       // ---- outcome
       const bool valid = go && pop_ok && contig;
       if (go) {
@@ -886,6 +1052,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         }
         accepted = valid & (((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u) != 0u);
       }
+      STAMP(8);  // outcome, accept rule
       if (p.trace != nullptr && valid && q == 0)
         p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
       n_steps += valid ? 1u : 0u;
@@ -917,6 +1084,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x112, 0xF, 0xF, true);
       dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x114, 0xF, 0xF, true);
       const int dnp = (int)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x154, 0xF, 0xF, false);  // row_newbcast:4
+      STAMP(9);  // commit
       if (accepted) {
         n_acc += 1;
         if (FULL && p.sched) sched_row(n_acc);
@@ -934,7 +1102,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         }
       }
       observe(valid);
-      STAMP(5);  // outcome, Metropolis, commit, observe
+      STAMP(5);  // counters, observe
     }
 
     STAMP(6);  // loop exit
@@ -1004,10 +1172,10 @@ int round16i(int x) { return (x + 15) / 16 * 16; }
 
 #ifdef FW_STAMPS
 extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
     return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

@@ -21,17 +21,19 @@ ch = Chains(dg, 65536, 4, block_seed(n, n, 2, 2), proposal="pairs",
             pop_bounds=population_bounds(n * n, 4, 0.05), base=2.63815853, seed=0)
 ch.run(1000)
 ch.run(1000)
-buf = np.zeros(8, np.uint64)
+buf = np.zeros(16, np.uint64)
 L.fw_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), 1)
+att0 = int(ch.stats()["attempts"].sum())
 for _ in range(3):
     ch.run(1000)
 L.fw_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), 0)
-names = ["draw", "select L1", "select L2", "gather+pop", "ring+search", "commit+observe",
-         "loop exit", "-"]
-tot = buf[:7].sum()
+names = ["draw", "select L1", "select L2", "gather+pop", "exact search", "counters+observe",
+         "loop exit", "ring+7x7 window", "outcome+accept", "commit"]
+tot = buf[:10].sum()
 st = ch.stats()
 print("kernel ms/launch (stamped):", ch.last_kernel_ms())
-iters = st["attempts"].sum() / 4  # rough: 4 chains per wave iteration
+iters = (int(st["attempts"].sum()) - att0) / 4  # rough: 4 chains per wave iteration
+print(f"7x7 window runs per wave-iter {buf[12] / iters:.3f}, flood iterations per run {buf[13] / max(buf[12], 1):.2f}")
 for nm, v in zip(names, buf):
     if v:
-        print(f"{nm:16s} {v / tot * 100:6.2f} %")
+        print(f"{nm:16s} {v / tot * 100:6.2f} %  {v / iters:8.1f} clk/wave-iter")

@@ -149,9 +149,15 @@ def _run_vs_oracle(case, n_chains, steps_list, seed=99, id0=3):
 
 
 @pytest.mark.parametrize("name", ["grid20_k4_mu", "grid16x24_k8", "grid30x18_k2_bi"])
-def test_many_chains_per_workgroup(gpu_lib, name, monkeypatch):
-    """77 chains: several waves and workgroups, contended search lock, a ragged last wave."""
+@pytest.mark.parametrize("bitboard", [True, False])
+def test_many_chains_per_workgroup(gpu_lib, name, bitboard, monkeypatch):
+    """77 chains: several waves and workgroups, a ragged last wave; exact searches in the
+    bitboard form (2-bit labels) and as the list search under the contended lock."""
     monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    if bitboard:
+        monkeypatch.delenv("FLIPWALK_NO_BITBOARD", raising=False)
+    else:
+        monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
     case = {c.name: c for c in CASES}[name]
     st = _run_vs_oracle(case, 77, [300, 500])
     assert st["bfs_runs"].sum() > 0
@@ -161,8 +167,10 @@ def test_many_chains_per_workgroup(gpu_lib, name, monkeypatch):
                                        ("grid30x18_k2_bi", "auto"), ("sec11_a2_k2", "auto"),
                                        ("tract_k4", "auto")])
 def test_search_list_spill(gpu_lib, name, path, monkeypatch):
-    """A 2-entry LDS visit list: every exact search spills to its HBM slice."""
+    """A 2-entry LDS visit list: every exact search spills to its HBM slice (the grid
+    kernel's bitboard search is switched off so that its list search runs)."""
     monkeypatch.setenv("FLIPWALK_LIST_CAP", "2")
+    monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
     if path == "wave64":
         monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
     else:
