@@ -275,6 +275,175 @@ struct Hood {
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
+// the value of the previous / next lane (wave_shr:1 / wave_shl:1 DPP; 0 at the wave's ends)
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, true);
+}
+// cells of X and their 4-neighbours (lane = grid row, bit = column)
+__device__ __forceinline__ uint32_t dilate32(uint32_t x) {
+  return x | (x << 1) | (x >> 1) | from_prev_lane(x) | from_next_lane(x);
+}
+
+// 32 bits "label == a" of the 32 nodes x0 .. x0+31 of a packed LB-bit label array of n
+// nodes.  Words before the array (x0 < 0) or past it are read at clamped positions: they
+// hold only nodes < 0 or >= n, which the caller masks.
+template <int LB>
+__device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int x0, uint32_t a) {
+  const LDS uint32_t* w = reinterpret_cast<const LDS uint32_t*>(lab);
+  const int bit = x0 * LB;
+  const int wi = bit >> 5;  // arithmetic
+  const uint32_t sh = (uint32_t)bit & 31u;
+  const int wlast = (n * LB - 1) >> 5;
+  uint32_t wd[LB + 1];
+#pragma unroll
+  for (int j = 0; j <= LB; ++j) wd[j] = w[min(max(wi + j, 0), wlast)];
+  uint32_t out = 0;
+#pragma unroll
+  for (int j = 0; j < LB; ++j) {  // 32 / LB labels per aligned dword
+    const uint32_t x = __builtin_amdgcn_alignbit(wd[j + 1], wd[j], sh);
+    uint32_t e;
+    if constexpr (LB == 2) {
+      const uint32_t y = x ^ (a * 0x55555555u);
+      e = ~(y | (y >> 1)) & 0x55555555u;
+      e = (e | (e >> 1)) & 0x33333333u;
+      e = (e | (e >> 2)) & 0x0F0F0F0Fu;
+      e = (e | (e >> 4)) & 0x00FF00FFu;
+      e = (e | (e >> 8)) & 0x0000FFFFu;
+    } else if constexpr (LB == 4) {
+      const uint32_t y = x ^ (a * 0x11111111u);
+      e = ~(y | (y >> 1) | (y >> 2) | (y >> 3)) & 0x11111111u;
+      e = (e | (e >> 3)) & 0x03030303u;
+      e = (e | (e >> 6)) & 0x000F000Fu;
+      e = (e | (e >> 12)) & 0x000000FFu;
+    } else {
+      static_assert(LB == 8, "labels are 2, 4 or 8 bits");
+      const uint32_t y = x ^ (a * 0x01010101u);
+      e = (~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u) >> 7;
+      e = (e | (e >> 7)) & 0x00030003u;
+      e = (e | (e >> 14)) & 0x0000000Fu;
+    }
+    out |= e << (j * (32 / LB));
+  }
+  return out;
+}
+
+// The exact race search of single_flip_contiguous (fw_device.h Ctx::race_search, the
+// oracle's contiguous_after) on bitboards, for row-major grids: a 64-row x 32-column
+// window around v, lane i = grid row vr - 32 + i, bit b = column vc - 16 + b, one u32 of
+// a-labelled cells (v excluded) per lane.  Level by level it holds the sets the list
+// search builds: per source direction d (0 up, 1 left, 2 right, 3 down) the frontier
+// cells reached from d, and the cells new at the next level.  Two classes merge when a
+// frontier cell of one is adjacent to a frontier cell or to a new cell of the other:
+// exactly the merges the list search makes, whatever its claim order.  The stopping rules
+// are the list search's, so the verdict and the counters (cells of the processed levels,
+// their degrees) equal its own.  No scratch, no lock, one VGPR per set.  am4: source
+// directions; lk: ring links pre-merged (bit 0 N-E, 1 E-S, 2 S-W, 3 W-N).  Returns -1
+// (nothing counted) when a frontier about to be processed holds a window-edge cell whose
+// outward neighbour is on the grid: the caller then runs the list search.
+template <int LB>
+__device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lane, int vr,
+                            int vc, uint32_t a, uint32_t am4, uint32_t lk, uint64_t& bfs_nodes,
+                            uint64_t& bfs_deg) {
+  const int r = vr - 32 + lane, c0 = vc - 16;
+  const bool rin = (r >= 0) & (r < H);
+  uint32_t A = eq_bits32<LB>(lab, n, (rin ? r : vr) * W + c0, a);
+  const int lo_cut = c0 < 0 ? -c0 : 0;  // bits of columns < 0
+  const int hi_n = W - c0;              // bits >= hi_n: columns >= W (hi_n >= 17)
+  uint32_t cm = ~0u << lo_cut;
+  if (hi_n < 32) cm &= (1u << hi_n) - 1u;
+  A &= rin ? cm : 0u;
+  if (lane == 32) A &= ~(1u << 16);  // v
+  // window-edge cells with an on-grid neighbour outside the window
+  uint32_t E = ((lane == 0) & (r > 0)) | ((lane == 63) & (r < H - 1)) ? ~0u : 0u;
+  if (c0 > 0) E |= 1u;
+  if (c0 + 31 < W - 1) E |= 1u << 31;
+  E &= A;
+  // frontier per direction; sources up (31, 16), left (32, 15), right (32, 17), down (33, 16)
+  uint32_t F[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int sl = d == 0 ? 31 : (d == 3 ? 33 : 32), sb = d == 1 ? 15 : (d == 2 ? 17 : 16);
+    F[d] = (lane == sl && ((am4 >> d) & 1u)) ? (1u << sb) : 0u;
+  }
+  // class of direction d: 4-bit member mask at bits 4d (uniform)
+  uint32_t M = 0x8421u;
+  auto unite = [&](int i, int j) {
+    const uint32_t m = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if ((m >> d) & 1u) M = (M & ~(15u << (4 * d))) | (m << (4 * d));
+  };
+  if (lk & 1u) unite(0, 2);  // N-E
+  if (lk & 2u) unite(2, 3);  // E-S
+  if (lk & 4u) unite(3, 1);  // S-W
+  if (lk & 8u) unite(1, 0);  // W-N
+  auto n_classes = [&]() {
+    int nc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      nc += (int)(((am4 >> d) & 1u) && (__ffs((M >> (4 * d)) & 15u) - 1) == d);
+    return nc;
+  };
+  uint32_t V = F[0] | F[1] | F[2] | F[3];
+  int verdict = -1;
+  uint32_t P;  // processed cells
+  for (;;) {
+    const uint32_t lvl = F[0] | F[1] | F[2] | F[3];
+    if (n_classes() == 1) {
+      verdict = 1;
+      P = V & ~lvl;
+      break;
+    }
+    if (ballot((lvl & E) != 0u)) return -1;
+    uint32_t D[4], nw = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      D[d] = ((am4 >> d) & 1u) ? dilate32(F[d]) & A : 0u;
+      nw |= D[d];
+    }
+    nw &= ~V;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 4; ++j) {
+        if (!((am4 >> i) & 1u) || !((am4 >> j) & 1u) || ((M >> (4 * i + j)) & 1u)) continue;
+        if (ballot((D[i] & (F[j] | (D[j] & nw))) != 0u)) unite(i, j);
+      }
+    uint32_t reach = 0;  // directions with a new cell
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      F[d] = D[d] & nw;
+      reach |= ballot(F[d] != 0u) ? (1u << d) : 0u;
+    }
+    P = V;
+    if (n_classes() == 1) {
+      verdict = 1;
+      break;
+    }
+    // a class none of whose directions reached a new cell is closed: disconnected
+    bool closed = false;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      closed |= ((am4 >> d) & 1u) && (reach & (M >> (4 * d)) & 15u) == 0u;
+    if (closed) {
+      verdict = 0;
+      break;
+    }
+    V |= nw;
+  }
+  // counters over the processed cells: degree = on-grid 4-neighbours
+  const uint32_t pc = (uint32_t)__popc(P);
+  uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
+  if (c0 <= 0) dg -= (P >> (-c0)) & 1u;          // column 0
+  if (hi_n <= 32) dg -= (P >> (hi_n - 1)) & 1u;  // column W - 1
+  bfs_nodes += wave_sum(pc);
+  bfs_deg += wave_sum(dg);
+  return verdict;
+}
+
 // E16: a general graph of max degree <= 16 whose adjacency rows are read from the padded
 // 16-wide table (four 16-byte loads in flight together) instead of walking CSR entries.
 template <int LB, bool GRID, bool E16 = false>
@@ -287,6 +456,7 @@ struct Ctx {
   GLB uint32_t* spill; // HBM part (this workgroup's slice)
   int32_t qcap, k;
   int lane;
+  bool bb;  // grids: exact searches try the bitboard form first
   int my_dr, my_dc;
 
   __device__ void init_roles() {
@@ -718,6 +888,18 @@ struct Ctx {
         const uint64_t A = (b48 & ((1ull << 24) - 1ull)) | ((b48 >> 24) << 25);
         const int wv = window_verdict(A);
         if (wv >= 0) return wv == 1;
+      }
+      if (bb) {  // bitboard search first; the list search past its window
+        int vr, vc;
+        divmod(v, vr, vc);
+        const int wv = grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a,
+                                        (uint32_t)(am >> 1) & 15u,
+                                        (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)),
+                                        bfs_nodes, bfs_deg);
+        if (wv >= 0) {
+          bfs_runs += 1;
+          return wv == 1;
+        }
       }
       // pre-merge the ring links
       if (lNE) merge(sx(1), sx(3));

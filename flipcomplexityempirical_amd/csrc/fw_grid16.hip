@@ -395,145 +395,6 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
   return verdict == 1;
 }
 
-// the value of the previous / next lane (wave_shr:1 / wave_shl:1 DPP; 0 at the wave's ends)
-__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, true);
-}
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, true);
-}
-// cells of X and their 4-neighbours (lane = grid row, bit = column)
-__device__ __forceinline__ uint32_t dilate32(uint32_t x) {
-  return x | (x << 1) | (x >> 1) | from_prev_lane(x) | from_next_lane(x);
-}
-
-// grid_race on bitboards (2-bit labels): a 64-row x 32-column window around v, lane i =
-// grid row vr - 32 + i, bit b = column vc - 16 + b, one u32 of a-labelled cells (v
-// excluded) per lane.  Level by level it holds the sets the list search builds: per
-// source direction d (0 up, 1 left, 2 right, 3 down) the frontier cells reached from d,
-// and the cells new at the next level.  Two classes merge when a frontier cell of one is
-// adjacent to a frontier cell or to a new cell of the other: exactly the merges the list
-// search makes, whatever its claim order.  The stopping rules are the list search's, so
-// the verdict and the counters (cells of the processed levels, their degrees) equal its
-// own and the oracle's contiguous_after.  No scratch, no lock, one VGPR per set.
-// Returns -1 (nothing counted) when a frontier about to be processed holds a window-edge
-// cell whose outward neighbour is on the grid: the caller then runs grid_race.
-__device__ int grid_race_bb(const LDS uint8_t* lab, int W, int H, int lane, int vr, int vc,
-                            uint32_t a, uint32_t am4, uint32_t lk, uint64_t& bfs_nodes,
-                            uint64_t& bfs_deg) {
-  const int r = vr - 32 + lane, c0 = vc - 16;
-  const bool rin = (r >= 0) & (r < H);
-  // 64 label bits from column c0 of row r (c0 >= -16: at most 4 B in front of the row,
-  // i.e. the 16-B guard or the previous slot; past the end the group sums; all masked)
-  const int bit = (mulW(rin ? r : vr, W) + c0) * 2;
-  const LDS uint32_t* wp = reinterpret_cast<const LDS uint32_t*>(lab) + (bit >> 5);
-  const uint32_t sh = (uint32_t)bit & 31u;
-  const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
-  const uint32_t pat = a * 0x55555555u;
-  auto eq16 = [&](uint32_t d) {  // 16 labels -> 16 bits "label == a"
-    const uint32_t x = d ^ pat;
-    uint32_t e = ~(x | (x >> 1)) & 0x55555555u;
-    e = (e | (e >> 1)) & 0x33333333u;
-    e = (e | (e >> 2)) & 0x0F0F0F0Fu;
-    e = (e | (e >> 4)) & 0x00FF00FFu;
-    return (e | (e >> 8)) & 0x0000FFFFu;
-  };
-  uint32_t A = eq16(__builtin_amdgcn_alignbit(w1, w0, sh)) |
-               (eq16(__builtin_amdgcn_alignbit(w2, w1, sh)) << 16);
-  const int lo_cut = c0 < 0 ? -c0 : 0;  // bits of columns < 0
-  const int hi_n = W - c0;              // bits >= hi_n: columns >= W (hi_n >= 17)
-  uint32_t cm = ~0u << lo_cut;
-  if (hi_n < 32) cm &= (1u << hi_n) - 1u;
-  A &= rin ? cm : 0u;
-  if (lane == 32) A &= ~(1u << 16);  // v
-  // window-edge cells with an on-grid neighbour outside the window
-  uint32_t E = ((lane == 0) & (r > 0)) | ((lane == 63) & (r < H - 1)) ? ~0u : 0u;
-  if (c0 > 0) E |= 1u;
-  if (c0 + 31 < W - 1) E |= 1u << 31;
-  E &= A;
-  // frontier per direction; sources up (31, 16), left (32, 15), right (32, 17), down (33, 16)
-  uint32_t F[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int sl = d == 0 ? 31 : (d == 3 ? 33 : 32), sb = d == 1 ? 15 : (d == 2 ? 17 : 16);
-    F[d] = (lane == sl && ((am4 >> d) & 1u)) ? (1u << sb) : 0u;
-  }
-  // class of direction d: 4-bit member mask at bits 4d (uniform)
-  uint32_t M = 0x8421u;
-  auto unite = [&](int i, int j) {
-    const uint32_t m = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      if ((m >> d) & 1u) M = (M & ~(15u << (4 * d))) | (m << (4 * d));
-  };
-  if (lk & 1u) unite(0, 2);  // N-E
-  if (lk & 2u) unite(2, 3);  // E-S
-  if (lk & 4u) unite(3, 1);  // S-W
-  if (lk & 8u) unite(1, 0);  // W-N
-  auto n_classes = [&]() {
-    int nc = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      nc += (int)(((am4 >> d) & 1u) && (__ffs((M >> (4 * d)) & 15u) - 1) == d);
-    return nc;
-  };
-  uint32_t V = F[0] | F[1] | F[2] | F[3];
-  int verdict = -1;
-  uint32_t P;  // processed cells
-  for (;;) {
-    const uint32_t lvl = F[0] | F[1] | F[2] | F[3];
-    if (n_classes() == 1) {
-      verdict = 1;
-      P = V & ~lvl;
-      break;
-    }
-    if (ballot((lvl & E) != 0u)) return -1;
-    uint32_t D[4], nw = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      D[d] = ((am4 >> d) & 1u) ? dilate32(F[d]) & A : 0u;
-      nw |= D[d];
-    }
-    nw &= ~V;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = i + 1; j < 4; ++j) {
-        if (!((am4 >> i) & 1u) || !((am4 >> j) & 1u) || ((M >> (4 * i + j)) & 1u)) continue;
-        if (ballot((D[i] & (F[j] | (D[j] & nw))) != 0u)) unite(i, j);
-      }
-    uint32_t reach = 0;  // directions with a new cell
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      F[d] = D[d] & nw;
-      reach |= ballot(F[d] != 0u) ? (1u << d) : 0u;
-    }
-    P = V;
-    if (n_classes() == 1) {
-      verdict = 1;
-      break;
-    }
-    // a class none of whose directions reached a new cell is closed: disconnected
-    bool closed = false;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      closed |= ((am4 >> d) & 1u) && (reach & (M >> (4 * d)) & 15u) == 0u;
-    if (closed) {
-      verdict = 0;
-      break;
-    }
-    V |= nw;
-  }
-  // counters over the processed cells: degree = on-grid 4-neighbours
-  const uint32_t pc = (uint32_t)__popc(P);
-  uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
-  if (c0 <= 0) dg -= (P >> (-c0)) & 1u;                // column 0
-  if (hi_n <= 32) dg -= (P >> (hi_n - 1)) & 1u;        // column W - 1
-  bfs_nodes += wave_sum(pc);
-  bfs_deg += wave_sum(dg);
-  return verdict;
-}
-
 // FULL = false: the lean instantiation for the common configuration (cut_accept, no
 // spatial maps), which then costs no registers for the optional features.
 template <int LB, int MODE, int PER, bool FULL>
@@ -942,8 +803,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         uint64_t bn = 0, bd = 0;
         int verdict = -1;
         if (LB == 2 && !p.no_bb)  // bitboard form first; the list search past its window
-          verdict = grid_race_bb(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, W, H, lane,
-                                 rdl(vr, L0), rdl(vc, L0), aa, am4, lk, bn, bd);
+          verdict = grid_race_bb<2>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, n, W, H,
+                                    lane, rdl(vr, L0), rdl(vc, L0), aa, am4, lk, bn, bd);
         if (verdict >= 0) {
           if (row == rr) {
             contig = verdict == 1;

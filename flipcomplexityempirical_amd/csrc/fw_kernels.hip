@@ -41,6 +41,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void fw
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.qcap = p.qcap;
   C.k = p.k;
+  C.bb = true;
+  C.bb = !p.no_bb;
   C.init_roles();
   const int lane = C.lane;
   const int n = p.g.n;
@@ -331,6 +333,7 @@ __global__ __launch_bounds__(64) void fw_eval_kernel(FwEvalParams p) {
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.qcap = p.qcap;
   C.k = p.k;
+  C.bb = true;
   C.init_roles();
   const int lane = C.lane;
   for (int i = blockIdx.x; i < p.m; i += gridDim.x) {

@@ -301,3 +301,57 @@ def test_step_schedule_bit_exact(gpu_lib, name, rule, path, monkeypatch):
         for f in ("attempts", "steps", "accepts", "sum_cut", "bnodes"):
             assert st[f][i] == ost[f][0], (name, i, f)
     assert st["accepts"].min() > 50  # the chains did move through the schedule
+
+
+def _corridor_plan(h, w, k, vertical):
+    """District 1: two blobs joined by a one-cell corridor far longer than the bitboard
+    window (32 columns / 64 rows); district 0 around them; districts 2.. as corner blocks."""
+    H, W = h, w
+    lab = np.zeros((H, W), np.int16)
+    mid = H // 2
+    lab[mid - 5:mid + 6, 2:10] = 1
+    lab[mid - 5:mid + 6, W - 10:W - 2] = 1
+    lab[mid, 10:W - 10] = 1
+    for t in range(2, k):  # small blocks along the top edge
+        lab[0:2, 4 * (t - 2) + 12:4 * (t - 2) + 15] = t
+    return np.ascontiguousarray(lab.T if vertical else lab).reshape(-1)
+
+
+@pytest.mark.parametrize("k,vertical,path", [(2, False, "auto"), (2, True, "auto"),
+                                             (2, False, "wave64"), (6, True, "wave64"),
+                                             (6, False, "auto")])
+def test_bitboard_window_escape(gpu_lib, k, vertical, path, monkeypatch):
+    """Searches along a corridor longer than the bitboard window leave it: the kernels fall
+    back to the list search.  Verdicts (fw_eval_flips) and whole chains (plans, search
+    counters) against the oracle."""
+    from flipcomplexityempirical_amd.graph import grid_graph
+    monkeypatch.delenv("FLIPWALK_NO_BITBOARD", raising=False)
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    h, w = 30, 120
+    g = grid_graph(w, h) if vertical else grid_graph(h, w)
+    init = _corridor_plan(h, w, k, vertical)
+    assert O.plan_valid(g, init, k, 1, g.n)
+    dg = DeviceGraph(g)
+    # every corridor cell flipped to district 0
+    v = np.flatnonzero(init == 1).astype(np.int32)
+    t = np.zeros(len(v), np.int16)
+    got = np.stack(eval_flips(dg, init, k, v, t, (1, g.n)), 1).astype(np.int32)
+    want = np.stack(O.eval_flips(g, init, k, v, t, 1, g.n), 1).astype(np.int32)
+    assert np.array_equal(got, want)
+    assert (got[:, 1] == 0).sum() > 50  # corridor cells disconnect district 1
+    # chains from the corridor plan: many searches run past the window
+    from flipcomplexityempirical_amd.chain import metropolis_table
+    thr = metropolis_table(1.0, g.maxdeg)
+    n_chains, steps, seed = 21, 150, 5
+    ch = Chains(dg, n_chains, k, init, proposal="pairs", pop_bounds=(1, g.n), base=1.0, seed=seed)
+    ch.run(steps)
+    labs, st = ch.labels(), ch.stats()
+    for i in range(n_chains):
+        olab, ost, _, _ = O.run_chain(g, init, k, 1, 1, g.n, thr, seed, i, steps)
+        assert np.array_equal(labs[i], olab), i
+        for f in ("attempts", "steps", "accepts", "contig_fail", "bfs_runs", "bfs_nodes", "bfs_deg"):
+            assert int(st[f][i]) == int(ost[f][0]), (i, f, st[f][i], ost[f][0])
+    assert (st["bfs_nodes"] > 40 * st["bfs_runs"]).any()  # searches far past the window
