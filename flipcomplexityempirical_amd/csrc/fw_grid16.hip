@@ -50,6 +50,7 @@ __device__ unsigned long long g_stamps[16];
 namespace {
 
 constexpr int ROW = 16;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr int MAX_NW = 4;          // waves per workgroup
 constexpr uint32_t SCR_BLOCK = 15;  // scratch code of v during a search
 constexpr int LDS_GUARD = 16;       // bytes in front of the first chain slot
@@ -265,11 +266,15 @@ __device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bo
   const int sb = q == 0 ? 17 : q == 1 ? 23 : q == 2 ? 25 : 31;
   uint64_t x = (need && q < 4) ? src & (1ull << sb) : 0ull;
   if (x) {
+    // two dilations per convergence test (same fixpoint, half the loop-exit tests)
     for (;;) {
       const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
-      if (y == x) break;
-      x = y;
+      x = (y | ((y << 1) & ~C0) | ((y >> 1) & ~C6) | (y >> 7) | (y << 7)) & A;
       FLOOD_COUNT;
+      if (x == y) break;
+#ifdef FW_VAR_FLOOD3
+      x = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
+#endif
     }
   }
   const uint32_t full = rowbits(ballot(x != 0ull && (x & src) == src), row);
@@ -608,7 +613,11 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         const uint32_t w2 = gsum[wi];  // words past GW are zero padding
         gs[2 * t] = w2 & 0xFFFFu;
         gs[2 * t + 1] = w2 >> 16;
+#ifdef FW_VAR_DOT2
+        s = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w2), u16x2{1, 1}, s, false);
+#else
         s += gs[2 * t] + gs[2 * t + 1];
+#endif
       }
       const uint32_t incl = row_scan(s);
       const uint32_t rb1 = rowbits(ballot(incl > r), row);
