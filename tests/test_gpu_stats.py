@@ -5,13 +5,17 @@ properties of the BASELINE configurations.
   40x40, k=4, 4,096 chains) against >= 256 oracle chains on DISJOINT Philox streams
   (independent samples), at matched step counts S in {10^3, 10^4}: two-sample KS at
   alpha = 0.01 and means within 3 combined standard errors, plus the per-chain time
-  averages (sum over yields / yields).
+  averages (sum over yields / yields).  The same at the C3 shape (100x100, 65,536 GPU
+  chains vs 256 oracle chains) at S in {10^3, 10^4, 10^5}; C2 also at 10^5.
 * C3 (100x100, k=4, 65,536 chains, the bench workload): counters, histogram moments and
   recomputed cut/boundary/population/contiguity of a subsample of final plans, and a
   spread of chain ids re-run on the oracle bit for bit.
 * Sharding: splitting the chain-id range over several handles (as ranks do) gives
   bit-identical merged histograms and stats.
 """
+import os
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 import pytest
 from scipy import stats as sps
@@ -27,7 +31,10 @@ MU = 2.63815853
 
 def _oracle_marginals(g, init, k, mode, bounds, base, seed, ids, steps):
     thr = metropolis_table(base, g.maxdeg)
-    st = [O.run_chain(g, init, k, mode, *bounds, thr, seed, cid, steps)[1][0] for cid in ids]
+    # ctypes releases the GIL: independent oracle chains run on a thread pool
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        st = list(ex.map(lambda cid: O.run_chain(g, init, k, mode, *bounds, thr, seed, cid,
+                                                 steps)[1][0], ids))
     return np.array(st)
 
 
@@ -38,7 +45,7 @@ def _compare(a, b, what):
     assert abs(a.mean() - b.mean()) < 3 * se + 1e-12, (what, a.mean(), b.mean(), se)
 
 
-@pytest.mark.parametrize("steps", [1000, 10000])
+@pytest.mark.parametrize("steps", [1000, 10000, 100000])
 @pytest.mark.parametrize("proposal,mode", [("pairs", 1), ("cutedge", 2)])
 def test_c2_marginals_match_independent_oracle_chains(gpu_lib, steps, proposal, mode):
     n, k, seed = 40, 4, 5
@@ -57,6 +64,27 @@ def test_c2_marginals_match_independent_oracle_chains(gpu_lib, steps, proposal, 
         _compare(gst[f] / gst["yields"], ost[f] / ost["yields"], f)
     # the yield histograms are the union of the per-chain yields
     assert ch.hist_cut().sum() == gst["yields"].sum() == 4096 * (steps + 1)
+
+
+@pytest.mark.parametrize("steps", [1000, 10000, 100000])
+def test_c3_marginals_match_independent_oracle_chains(gpu_lib, steps):
+    """SURVEY.md §8(d) at the bench shape: 65,536 GPU chains vs 256 oracle chains."""
+    n, k, seed = 100, 4, 7
+    g = grid_graph(n, n)
+    init = block_seed(n, n, 2, 2)
+    bounds = population_bounds(g.total_pop, k, 0.05)
+    ch = Chains(DeviceGraph(g), 65536, k, init, proposal="pairs", pop_bounds=bounds, base=MU,
+                seed=seed)
+    ch.run(steps)
+    gst = ch.stats()
+    assert not gst["stuck"].any()
+    ost = _oracle_marginals(g, init, k, 1, bounds, MU, seed, range(1 << 20, (1 << 20) + 256),
+                            steps)
+    for f in ("cut", "bnodes"):
+        _compare(gst[f].astype(float), ost[f].astype(float), f)
+    for f in ("sum_cut", "sum_bnodes"):
+        _compare(gst[f] / gst["yields"], ost[f] / ost["yields"], f)
+    assert ch.hist_cut().sum() == gst["yields"].sum() == 65536 * (steps + 1)
 
 
 def test_c3_full_size_properties(gpu_lib):
