@@ -24,6 +24,9 @@
 // bit for bit (tests/test_gpu_parity.py).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "fw_device.h"
 
 namespace {
@@ -466,8 +469,39 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   int per_cu = 0;
   e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, (size_t)p.lds_bytes);
   if (e != hipSuccess || per_cu <= 0) return -1;
+  // LDS-bound residency (C5: 23.5 KB per chain, 6 per CU): shorten the LDS visit list,
+  // down to 128 entries (longer searches continue in the HBM spill area), when that keeps
+  // one more chain per CU; the longest list that reaches the best residency is kept.
+  // FLIPWALK_LIST_CAP pins the length (tests of the spill path).
+  const char* cap_env = getenv("FLIPWALK_LIST_CAP");
+  if (!(cap_env && cap_env[0]) && p.qcap > 128) {
+    const int base = p.off_list;
+    int best_q = p.qcap, best = per_cu;
+    for (int q = p.qcap - 8; q >= 128; q -= 8) {
+      const int lds = base + 4 * q;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+        return -1;
+      int pc = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, fn, 64, (size_t)lds) != hipSuccess)
+        return -1;
+      if (pc > best) {
+        best = pc;
+        best_q = q;
+      }
+    }
+    p.qcap = best_q;
+    p.lds_bytes = base + 4 * best_q;
+    per_cu = best;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
+        hipSuccess)
+      return -1;
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
+  const char* verbose = getenv("FLIPWALK_VERBOSE");
+  if (verbose && verbose[0] == '1')
+    fprintf(stderr, "flipwalk: chain kernel LDS %d B (list %d), %d chains per CU\n", p.lds_bytes,
+            p.qcap, per_cu);
   long long gsz = (long long)per_cu * prop.multiProcessorCount;
   if (gsz > p.n_chains) gsz = p.n_chains;
   *grid = (int)(gsz < 1 ? 1 : gsz);
@@ -477,6 +511,9 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   if (p.use16) return fw_grid16_launch(p, grid, stream);
   void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G);
+  // handles of different graphs share instantiations: set this handle's LDS size
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) != hipSuccess)
+    return -1;
   void* args[] = {const_cast<FwRunParams*>(&p)};
   hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes, (hipStream_t)stream);
   return e == hipSuccess ? 0 : -1;
