@@ -106,6 +106,7 @@ struct fw_graph {
   int32_t* d_ew = nullptr;
   uint64_t* d_nbadj = nullptr;  // [nnz] (general graphs): adjacency among v's neighbours
   int32_t* d_ell = nullptr;     // [n][16] (general graphs, max degree <= 16): padded rows
+  double* d_invb = nullptr;     // [n+1] 1.0 / max(b, 1) for the Σ1/|B| observable
   int64_t popof(int x) const { return pop.empty() ? 1 : pop[x]; }
   FwGraphDev dev() const {
     FwGraphDev g;
@@ -115,6 +116,7 @@ struct fw_graph {
     g.nbadj = d_nbadj;
     g.ell = d_ell;
     g.pop = d_pop;
+    g.invb = d_invb;
     g.n = n;
     g.nedges = nnz / 2;
     g.maxdeg = maxdeg;
@@ -347,6 +349,10 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   }
   if (e3 == hipSuccess && !nbadj.empty())
     e3 = hipMalloc(&g->d_nbadj, sizeof(uint64_t) * nbadj.size());
+  // the kernels read 1/|B| here instead of dividing in fp64 on every accepted step
+  std::vector<double> invb((size_t)n + 1);
+  for (int b = 0; b <= n; ++b) invb[b] = 1.0 / (double)(b > 0 ? b : 1);
+  if (e3 == hipSuccess) e3 = hipMalloc(&g->d_invb, sizeof(double) * invb.size());
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
     fw_graph_destroy(g);
     return fail(FW_EHIP, "hipMalloc failed for graph");
@@ -362,6 +368,8 @@ int fw_graph_create(const int32_t* rowptr, const int32_t* col, const int64_t* po
   if (!nbadj.empty())
     up &= hipMemcpy(g->d_nbadj, nbadj.data(), sizeof(uint64_t) * nbadj.size(),
                     hipMemcpyHostToDevice) == hipSuccess;
+  up &= hipMemcpy(g->d_invb, invb.data(), sizeof(double) * invb.size(), hipMemcpyHostToDevice) ==
+        hipSuccess;
   if (!ell.empty())
     up &= hipMemcpy(g->d_ell, ell.data(), sizeof(int32_t) * ell.size(), hipMemcpyHostToDevice) ==
           hipSuccess;
@@ -390,6 +398,7 @@ void fw_graph_destroy(fw_graph* g) {
   if (g->d_ew) (void)hipFree(g->d_ew);
   if (g->d_nbadj) (void)hipFree(g->d_nbadj);
   if (g->d_ell) (void)hipFree(g->d_ell);
+  if (g->d_invb) (void)hipFree(g->d_invb);
   delete g;
 }
 

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       npairs = (int32_t)row_sum(np);
     }
     lds_order();
-    double invb = 1.0 / (double)(bnodes > 0 ? bnodes : 1);
+    double invb = p.g.invb[bnodes];  // 1/|B| from the graph's table, no fp64 divide
 
     // histogram windows: row-lane q counts values base+q and base+16+q
     uint32_t hc0 = 0, hc1 = 0, hb0 = 0, hb1 = 0;
@@ -904,6 +904,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const uint64_t b_plus = ballot(valid && mine && wo == 0 && wn > 0);
       const uint64_t b_minus = ballot(valid && mine && wo > 0 && wn == 0);
       const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
+      // 1/|B'| (read now, used after the accept rule and commit)
+      const double invb_new = p.g.invb[bnodes + plus - minus];
       // ---- accept rule (lane dcut+D holds the tabulated bound; include/flipwalk.h)
       bool accepted;
       if (rule == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
@@ -963,7 +965,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         cut += dcut;
         bnodes += plus - minus;
         n_bchg += (uint32_t)(plus + minus);
-        if (plus | minus) invb = 1.0 / (double)bnodes;
+        invb = invb_new;
         if ((uint32_t)q == a) pops -= pv;
         if ((uint32_t)q == d) pops += pv;
         if (rule == FW_ACCEPT_BOUNDARY && p.flags[v]) {

@@ -19,6 +19,7 @@ struct FwGraphDev {
   const uint64_t* nbadj;  // [nnz] entry (v, i): bit j set iff neighbours i and j of v are adjacent
   const int32_t* ell;     // [n][16] neighbours padded with -1 (general graphs, max degree <= 16)
   const int64_t* pop;     // [n] or nullptr (unit populations)
+  const double* invb;     // [n+1] 1.0 / max(b, 1), correctly rounded (no fp64 divide per step)
   int32_t n, nedges, maxdeg;
   int32_t gw, gh;         // grid width/height (gw == 0: general CSR)
   uint64_t gmagic;        // ceil(2^42 / gw): x / gw == (x * gmagic) >> 42 for x < 2^21

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void fw
       npairs = (int32_t)wave_sum(np);
     }
     lds_order();
-    double invb = 1.0 / (double)bnodes;
+    double invb = p.g.invb[bnodes];  // 1/|B| from the graph's table (|B| > 0 for k >= 2)
 
     // histogram windows: lane i counts value base+i
     uint32_t hc = 0, hb = 0;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void fw
         cut += dcut;
         bnodes += plus - minus;
         n_bchg += (uint32_t)(plus + minus);
-        if (plus | minus) invb = 1.0 / (double)bnodes;
+        if (plus | minus) invb = p.g.invb[bnodes];
         if (lane == (int)a) pops -= pv;
         if (lane == (int)d) pops += pv;
         if (p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
