@@ -501,13 +501,16 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       }
     };
     if (FULL && p.sched) sched_row(0);
-    uint64_t attempts = stp->attempts;
+    // attempts and yields of this launch in 32 bits: attempts = att0 + n_att, and every
+    // counted step is one yield (plus the initial state's on a chain's first launch)
+    const uint64_t att0 = stp->attempts;
+    uint32_t n_att = 0;
     const uint64_t yields0 = stp->yields;
     int32_t stuck = has ? stp->stuck : 1;
     int64_t sum_cut = stp->sum_cut, sum_bnodes = stp->sum_bnodes;
     double sum_invb = stp->sum_invb;
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0, n_sdeg = 0, n_adeg = 0, n_bchg = 0;
-    uint32_t n_yield = 0, retries = 0;
+    uint32_t retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
     Pend pend = maps_on ? pend_load(p, cc) : Pend{-1, 0, 0u};
     // boundary_node-flagged nodes of district q (FW_ACCEPT_BOUNDARY), lane q
@@ -548,7 +551,6 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     int32_t base_c = max(0, cut - 16), base_b = max(0, bnodes - 16);
     auto observe = [&](bool on) {
       if (!on) return;
-      n_yield += 1;
       sum_cut += cut;
       sum_bnodes += bnodes;
       sum_invb += invb;
@@ -573,7 +575,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       hb0 += ib == q;
       hb1 += ib == q + ROW;
     };
-    observe(has && !stuck && yields0 == 0 && attempts == 0);
+    const bool first = has && !stuck && yields0 == 0 && att0 == 0;
+    observe(first);
 
     // Philox batches: lane q of a row holds the draw of its chain's attempt (base + q).
     // Active rows consume one attempt per loop iteration in lockstep: each iteration
@@ -591,7 +594,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (ballot(act) == 0ull) break;
 
       if (bpos == ROW) {
-        const uint64_t t = attempts + (uint64_t)q;
+        const uint64_t t = att0 + (uint64_t)(n_att + (uint32_t)q);
         pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
                     in_vgpr(key0), in_vgpr(key1));
         bpos = 0;
@@ -600,7 +603,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const U4 x = {row_first(pb.x0), row_first(pb.x1), row_first(pb.x2), row_first(pb.x3)};
       pb = U4{row_shl1(pb.x0), row_shl1(pb.x1), row_shl1(pb.x2), row_shl1(pb.x3)};
       ++bpos;
-      attempts += act ? 1u : 0u;
+      n_att += act ? 1u : 0u;
       const uint32_t r = scale64(x.x0, x.x1, (uint32_t)(npairs > 0 ? npairs : 1));
 
       STAMP(0);  // draw
@@ -929,7 +932,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
       n_steps += valid ? 1u : 0u;
       if (maps_on && accepted) {  // spatial observables: fire-and-forget atomics
-        const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
+        // index of the new state's yield (n_steps already counts this step)
+        const int64_t t = (int64_t)(yields0 + (n_steps - 1u) + (first ? 1u : 0u));
         if (q >= 1 && q <= 4 && h.x >= 0 && (h.lx == a || h.lx == d)) {
           const int e = q == 1   ? grid_eid_down(vr - 1, vc, W, H)
                         : q == 2 ? grid_eid_right(vr, vc - 1, W, H)
@@ -991,7 +995,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
       if (q == 0 && maps_on) pend_store(p, c, pend);
       if (q == 0) {
-        stp->attempts = attempts;
+        stp->attempts = att0 + n_att;
         stp->steps += n_steps;
         stp->accepts += n_acc;
         stp->pop_fail += n_popf;
@@ -1002,7 +1006,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         stp->sum_deg += n_sdeg;
         stp->acc_deg += n_adeg;
         stp->n_bchg += n_bchg;
-        stp->yields += n_yield;
+        stp->yields += (uint64_t)n_steps + (first ? 1u : 0u);
         stp->sum_cut = sum_cut;
         stp->sum_bnodes = sum_bnodes;
         stp->sum_invb = sum_invb;
