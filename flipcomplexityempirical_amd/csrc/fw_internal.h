@@ -66,6 +66,7 @@ struct FwRunParams {
   int32_t off_scr, scr_bytes;  // 4-bit search scratch
   int32_t off_list16, qcap16;  // shared visit list
   int32_t no_bb;               // 1: exact searches skip the bitboard form (tests)
+  int32_t wpe5;                // 1: the 5-waves-per-SIMD chain-kernel instantiation
   int32_t lds16;               // dynamic LDS bytes per workgroup
   // spatial observables (nullptr: off).  Per chain c: acc [E] (int64: sum of -t when an
   // edge becomes cut and +t when it becomes uncut, so cut_times = acc + [cut now] * Y),

@@ -32,8 +32,9 @@
 namespace {
 
 // ---------------------------------------------------------------- the chain kernel
-template <int LB, bool GRID, int MODE, int PER, bool E16>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void fw_run_kernel(FwRunParams p) {
+// WPE: waves per SIMD the register budget targets (5 only where LDS admits 20 chains per CU)
+template <int LB, bool GRID, int MODE, int PER, bool E16, int WPE = 4>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void fw_run_kernel(FwRunParams p) {
   extern __shared__ __align__(16) uint8_t smem[];
   Ctx<LB, GRID, E16> C;
   C.g = p.g;
@@ -437,18 +438,21 @@ __global__ void fw_map_read_kernel(FwMapRead m) {
   }
 }
 
-template <int LB, bool GRID, int MODE, bool E16>
+template <int LB, bool GRID, int MODE, bool E16, int WPE = 4>
 void* pick_per(int G) {
-  if (G <= 64 * 2) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16>);
-  if (G <= 64 * 4) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16>);
-  if (G <= 64 * 8) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16>);
-  return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16>);
+  if (G <= 64 * 2) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE>);
+  if (G <= 64 * 4) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE>);
+  if (G <= 64 * 8) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE>);
+  return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE>);
 }
 
 // grids: implicit neighbours; general graphs: the padded 16-wide table when it exists
-void* pick_run(int lb, bool grid, bool e16, int mode, int G) {
+void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false) {
   const bool cut = mode == FW_PROPOSE_CUTEDGE;
   if (lb == 4) {
+    // small general graphs (4-bit labels, padded rows): a 5-waves-per-SIMD register budget
+    if (!grid && e16 && wpe5)
+      return cut ? pick_per<4, false, 2, true, 5>(G) : pick_per<4, false, 1, true, 5>(G);
     if (grid) return cut ? pick_per<4, true, 2, false>(G) : pick_per<4, true, 1, false>(G);
     if (e16) return cut ? pick_per<4, false, 2, true>(G) : pick_per<4, false, 1, true>(G);
     return cut ? pick_per<4, false, 2, false>(G) : pick_per<4, false, 1, false>(G);
@@ -496,6 +500,23 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
         hipSuccess)
       return -1;
   }
+  // 4-bit labels on padded rows: when LDS admits more chains per CU than the 4-wave
+  // register budget, the 5-wave instantiation (Frankengraph: 16 -> 20 chains per CU, +4%)
+  p.wpe5 = 0;
+  if (lb == 4 && p.g.gw == 0 && p.g.ell != nullptr) {
+    void* fn5 = pick_run(lb, false, true, p.mode, p.G, true);
+    if (hipFuncSetAttribute(fn5, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
+        hipSuccess)
+      return -1;
+    int pc5 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc5, fn5, 64, (size_t)p.lds_bytes) !=
+        hipSuccess)
+      return -1;
+    if (pc5 > per_cu) {
+      p.wpe5 = 1;
+      per_cu = pc5;
+    }
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
   const char* verbose = getenv("FLIPWALK_VERBOSE");
@@ -510,7 +531,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
 
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   if (p.use16) return fw_grid16_launch(p, grid, stream);
-  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G);
+  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0);
   // handles of different graphs share instantiations: set this handle's LDS size
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) != hipSuccess)
     return -1;
