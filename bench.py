@@ -2,10 +2,13 @@
 """bench.py — flip steps/sec of the batched single-node flip walk on MI355X.
 
 Workload (BASELINE.json configs[2], SURVEY.md §8d "C3"): 100x100 grid, k=4 districts
-seeded as 50x50 quadrants, 65,536 independent chains per GPU, proposal
+seeded as 50x50 quadrants, 65,536 independent chains IN TOTAL, sharded over the GPUs of
+the run (strong scaling: global chain ids distributed.shard_range(65536, N, rank), so at
+N = 1/2/4/8 each GPU runs 65,536 / 32,768 / 16,384 / 8,192 chains); proposal
 slow_reversible_propose over (node, foreign label) pairs (grid_chain_sec11.py:117-130),
 single_flip_contiguous + 5% population bound, Metropolis cut_accept with base
-mu = 2.63815853 (grid_chain_sec11.py:33,171-179).
+mu = 2.63815853 (grid_chain_sec11.py:33,171-179).  ``--scaling weak`` gives every GPU
+``--chains`` chains instead.
 
 A bench "step" is one kernel launch that advances every chain by --inner counted flip
 steps (valid proposals, MarkovChain counter increments); value = counted flip steps of
@@ -15,14 +18,16 @@ all chains on all ranks / max-over-ranks wall time of the K timed launches.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Extra fields: "roofline" (dominant kernel, algorithmic bytes of SURVEY.md §8d per launch /
-mean HIP-event launch time vs 8 TB/s) and "cpu_baseline" (the GerryChain-equivalent
-Python proxy, oracle/reference_proxy.py, one chain per process on the host cores, rank 0
-at N=1 only, bounded sample).
+mean HIP-event launch time vs 8 TB/s), "cpu_baseline" (the GerryChain-equivalent Python
+proxy, oracle/reference_proxy.py, one chain per process on every usable host core) and
+"cpu_native" (the C oracle, one chain per thread on the same cores), rank 0 at N=1 only,
+bounded samples of the same workload.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import multiprocessing as mp
 import os
 import sys
@@ -33,7 +38,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MU = 2.63815853
+from flipcomplexityempirical_amd.workloads import MU, ladder, workload  # noqa: E402,F401
+
 METRIC = "flip steps/sec (whole node), 100×100 grid k=4 batched chains; % HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -54,58 +60,40 @@ def totals(st):
     return {k: int(st[k].astype(np.uint64).sum()) for k in keys}
 
 
-# ------------------------------------------------------------------ workloads
-def ladder(n_bases=64, lo=0.1, hi=10.0):
-    """C5: Metropolis bases log-spaced over the reference's range (grid_chain_sec11.py:34)."""
-    return np.geomspace(lo, hi, n_bases)
+# ------------------------------------------------------------------ host description
+def host_cores():
+    """(usable cores, affinity cores, cgroup CPU quota in cores or None, os.cpu_count())."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    usable = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    return usable, aff, quota, os.cpu_count()
 
 
-def workload(name, grid=None, k=None):
-    """(graph, seed plan, k, proposal, base, percent, default chains/GPU, description).
-
-    c3 (default, BASELINE configs[2]) 100x100 grid, k=4 quadrants, 65,536 chains/GPU
-    c2 (configs[1])   40x40 grid, k=4 quadrants, 4,096 chains
-    c4 (configs[3])   9,000-node Delaunay dual graph, lognormal pops, k=18 tree seed
-    c5 (configs[4])   200x200 grid, k=8 (2x4 blocks), 1,024 chains per base of a 64-base
-                      ladder in [0.1, 10]; 8 bases (8,192 chains) per GPU
-    frank             the 5,000-node Frankengraph of Frankenstein_chain.py, k=2, bi proposal
-    """
-    from flipcomplexityempirical_amd.graph import (block_seed, delaunay_graph, frankenstein_graph,
-                                                   frankenstein_seed, grid_graph)
-    from flipcomplexityempirical_amd.seeds import tree_seed
-    if name in ("c3", "c2"):
-        n = grid or (100 if name == "c3" else 40)
-        kk = k or 4
-        g = grid_graph(n, n)
-        init = block_seed(n, n, 2, 2) if kk == 4 else block_seed(n, n, 2, kk // 2)
-        chains = 65536 if name == "c3" else 4096
-        return (g, init, kk, "pairs", MU, 0.05, chains,
-                f"{name.upper()}: {n}x{n} grid, k={kk} block seed")
-    if name == "c4":
-        g = delaunay_graph(9000, seed=0)
-        kk = k or 18
-        return (g, tree_seed(g, kk, 0.05), kk, "pairs", MU, 0.05, 16384,
-                f"C4: 9000-node Delaunay dual graph (lognormal pops), k={kk} tree seed")
-    if name == "c5":
-        n = grid or 200
-        g = grid_graph(n, n)
-        return (g, block_seed(n, n, 2, 4), 8, "pairs", None, 0.05, 8192,
-                f"C5: {n}x{n} grid, k=8 2x4 blocks, 64-base ladder [0.1,10] x 1024 chains")
-    if name == "frank":
-        g = frankenstein_graph()
-        return (g, frankenstein_seed(g, 0), 2, "bi", 1 / .379, 0.5, 16384,
-                "Frankengraph (Frankenstein_chain.py), k=2 diagonal seed, bi proposal")
-    raise ValueError(f"unknown workload {name}")
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-# ------------------------------------------------------------------ CPU baseline
+# ------------------------------------------------------------------ CPU baselines
 def _proxy_worker(args):
     name, percent, base, seed, cid, seconds = args
     sys.path.insert(0, ROOT)
     from flipcomplexityempirical_amd.chain import PROPOSALS
     from oracle.reference_proxy import ProxyChain
-    g, lab, k, proposal, _, _, _, _ = workload(name)
-    ch = ProxyChain(g, lab, k, PROPOSALS[proposal], percent, base, seed, cid)
+    w = workload(name)
+    ch = ProxyChain(w.graph, w.init, w.k, PROPOSALS[w.proposal], percent, base, seed, cid)
     ch.run(1)  # builds caches
     t0 = time.perf_counter()
     steps = 0
@@ -115,27 +103,63 @@ def _proxy_worker(args):
     return steps, time.perf_counter() - t0
 
 
+def _host_fields(workers):
+    usable, aff, quota, total = host_cores()
+    return {"cores": workers, "cpu_model": cpu_model(), "cpu_count": total,
+            "affinity_cores": aff, "cgroup_quota_cores": quota}
+
+
 def cpu_baseline(name, desc, percent, base, seed, seconds=10.0, workers=None):
-    workers = workers or min(16, os.cpu_count() or 1)
+    """The GerryChain-equivalent Python proxy, one chain per process on every usable core."""
+    workers = workers or host_cores()[0]
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers) as pool:
         res = pool.map(_proxy_worker, [(name, percent, base, seed, i, seconds)
                                        for i in range(workers)])
     rate = sum(s / t for s, t in res)
-    return {"value": rate, "unit": "flip steps/s", "cores": workers, "kind": "port",
-            "sample": f"GerryChain-equivalent Python proxy (oracle/reference_proxy.py): "
-                      f"{workers} chains x ~{seconds:.0f}s, one chain per process, same "
-                      f"workload ({desc}, base {base:.6g}, {percent:.0%} pop); "
-                      f"{sum(s for s, _ in res)} steps total"}
+    out = {"value": rate, "unit": "flip steps/s", "kind": "port",
+           "sample": f"GerryChain-equivalent Python proxy (oracle/reference_proxy.py): "
+                     f"{workers} chains x ~{seconds:.0f}s, one chain per process on every usable "
+                     f"host core, same workload ({desc}, base {base:.6g}, {percent:.0%} pop); "
+                     f"{sum(s for s, _ in res)} steps total"}
+    out.update(_host_fields(workers))
+    out["per_core"] = rate / workers
+    out["extrapolated_all_cpus"] = rate / workers * out["cpu_count"]
+    return out
 
 
-def native_cpu_rate(g, init, k, mode, percent, base, seed, steps=20000):
-    from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+def native_cpu_baseline(w, bounds, base, seed, seconds=10.0, workers=None):
+    """The C oracle (oracle/flipchain_oracle.c), one chain per thread on every usable core
+    (ctypes releases the GIL), each chain advanced in 5,000-step calls until the deadline."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from flipcomplexityempirical_amd.chain import PROPOSALS, metropolis_table
     from oracle import oracle as O
-    lo, hi = population_bounds(g.total_pop, k, percent)
-    t0 = time.perf_counter()
-    O.run_chain(g, init, k, mode, lo, hi, metropolis_table(base, g.maxdeg), seed, 0, steps)
-    return steps / (time.perf_counter() - t0)
+    workers = workers or host_cores()[0]
+    thr = metropolis_table(base, w.graph.maxdeg)
+    mode = PROPOSALS[w.proposal]
+
+    def one(cid):
+        lab, st = w.init.copy(), O.new_stats(1)
+        lab, st, _, _ = O.run_chain(w.graph, lab, w.k, mode, *bounds, thr, seed, cid, 100, stats=st)
+        t0 = time.perf_counter()
+        s0 = int(st["steps"][0])
+        while time.perf_counter() - t0 < seconds:
+            lab, st, _, _ = O.run_chain(w.graph, lab, w.k, mode, *bounds, thr, seed, cid, 5000,
+                                        stats=st)
+        return int(st["steps"][0]) - s0, time.perf_counter() - t0
+
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        res = list(ex.map(one, range(workers)))
+    rate = sum(s / t for s, t in res)
+    out = {"value": rate, "unit": "flip steps/s", "kind": "port",
+           "sample": f"C oracle (oracle/flipchain_oracle.c, the bit-exact restatement), "
+                     f"{workers} chains x ~{seconds:.0f}s, one chain per thread on every usable "
+                     f"host core, same workload; {sum(s for s, _ in res)} steps total"}
+    out.update(_host_fields(workers))
+    out["per_core"] = rate / workers
+    out["extrapolated_all_cpus"] = rate / workers * out["cpu_count"]
+    return out
 
 
 # ------------------------------------------------------------------ main
@@ -146,8 +170,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--inner", type=int, default=1000, help="flip steps per chain per launch")
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5", "frank"],
-                    help="workload (see workload()); the driver's line is the default c3")
-    ap.add_argument("--chains", type=int, default=None, help="chains per GPU (weak scaling)")
+                    help="workload (flipcomplexityempirical_amd/workloads.py); the driver's line "
+                         "is the default c3")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: --chains (default: the configuration's) in total, sharded; "
+                         "weak: --chains per GPU")
+    ap.add_argument("--chains", type=int, default=None)
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--base", type=float, default=None)
@@ -178,27 +206,29 @@ def main():
         torch.cuda.set_device(device)
         dist.init_process_group(args.backend)
     tdev = "cuda" if args.backend == "nccl" else "cpu"
-    from flipcomplexityempirical_amd.chain import (PROPOSALS, Chains, DeviceGraph,
-                                                   population_bounds)
-    from flipcomplexityempirical_amd.distributed import merge_histograms
+    from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bounds
+    from flipcomplexityempirical_amd.distributed import merge_histograms, shard_range
 
-    g, init, k, proposal, base, percent, chains, desc = workload(args.config, args.grid, args.k)
-    proposal = args.proposal or proposal
-    percent = args.percent if args.percent is not None else percent
-    chains = args.chains or chains
-    cid0 = rank * chains
-    if args.config == "c5" and args.base is None:
-        # whole 1,024-chain base groups per GPU: global chain id g runs ladder[g // 1024]
-        lad = ladder()
-        base = lad[(np.arange(cid0, cid0 + chains) // 1024) % len(lad)]
-        base_desc = f"ladder bases {lad[(cid0 // 1024) % 64]:.4g}..{base[-1]:.4g}"
+    w = workload(args.config, args.grid, args.k)
+    g, init, k = w.graph, w.init, w.k
+    proposal = args.proposal or w.proposal
+    percent = args.percent if args.percent is not None else w.percent
+    if args.scaling == "strong":
+        total = args.chains or w.chains
+        lo, hi = shard_range(total, world, rank)
     else:
-        base = args.base if args.base is not None else base
-        base_desc = f"base {base:.9g}"
+        per = args.chains or w.chains
+        total = per * world
+        lo, hi = rank * per, (rank + 1) * per
+    chains = hi - lo
+    if args.base is not None:
+        base, base_desc = args.base, f"base {args.base:.9g}"
+    else:
+        base, base_desc = w.bases(lo, hi), w.base_desc(0, total)
     bounds = population_bounds(g.total_pop, k, percent)
     dg = DeviceGraph(g, device=device)
     ch = Chains(dg, chains, k, init, proposal=proposal, pop_bounds=bounds, base=base,
-                seed=args.seed, chain_id0=cid0)
+                seed=args.seed, chain_id0=lo)
     if args.maps:
         ch.enable_maps([-1, 1] if k == 2 else None)
 
@@ -225,12 +255,13 @@ def main():
     d = {kk: st1[kk] - st0[kk] for kk in st1}
     steps_local = d["steps"]
     if dist is not None:
-        t = torch.tensor([dt, float(steps_local)], dtype=torch.float64, device=tdev)
+        t = torch.tensor([dt, float(steps_local), float(d["attempts"]), float(d["accepts"])],
+                         dtype=torch.float64, device=tdev)
         dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
-        dt, steps_all = float(t[0]), float(t[1])
+        dist.all_reduce(t[1:4], op=dist.ReduceOp.SUM)
+        dt, steps_all, att_all, acc_all = (float(x) for x in t)
     else:
-        steps_all = float(steps_local)
+        steps_all, att_all, acc_all = float(steps_local), float(d["attempts"]), float(d["accepts"])
     hist_cut, hist_b = merge_histograms(ch.hist_cut(), ch.hist_b(), dist)
 
     kernel_ms = float(np.mean(kms))
@@ -258,26 +289,38 @@ def main():
                      "rocprof_kernel_ms": (tj.get("kernel_trace") or {}).get("avg_ms")}
 
     if rank == 0:
+        if dist is None:
+            par = "1 GPU"
+        elif args.same_device:
+            par = (f"REHEARSAL: {world} ranks on ONE device (same device, {args.backend} "
+                   f"process group); chain ids sharded by shard_range, histograms merged by one "
+                   f"{args.backend} all-reduce")
+        else:
+            par = (f"{world} GPUs, one process each: chain ids sharded by shard_range (no "
+                   f"data-path collective), histograms merged by one "
+                   f"{'RCCL (nccl) all-reduce over xGMI' if args.backend == 'nccl' else 'gloo all-reduce'}")
         out = {
             "metric": METRIC,
             "value": steps_all / dt,
             "unit": "flip steps/s",
-            "n_gpus": world,
+            "n_gpus": 1 if args.same_device else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": f"{desc}, {chains} chains/GPU, {proposal} proposal, {base_desc}, "
-                            f"{percent:.0%} pop bound, contiguity",
+                "workload": f"{w.desc}, {total} chains in total ({chains} on rank 0), "
+                            f"{proposal} proposal, {base_desc}, {percent:.0%} pop bound, "
+                            f"contiguity",
+                "chains_total": total,
                 "chains_per_gpu": chains,
                 "spatial_maps": bool(args.maps),
                 "flip_steps_per_chain_per_step": args.inner,
-                "parallelism": f"chains sharded over {world} GPU(s), RCCL histogram merge",
+                "parallelism": par,
             },
             "roofline": {
                 "bound": "hbm",
@@ -289,8 +332,8 @@ def main():
             },
             "issue_roofline": issue,
             "kernel_ms": kernel_ms,
-            "proposals_per_s": d["attempts"] * world / dt,
-            "accepts_per_s": d["accepts"] * world / dt,
+            "proposals_per_s": att_all / dt,
+            "accepts_per_s": acc_all / dt,
             "valid_frac": d["steps"] / max(1, d["attempts"]),
             "accept_frac": d["accepts"] / max(1, d["steps"]),
             "bfs_runs_per_step": d["bfs_runs"] / max(1, d["steps"]),
@@ -302,10 +345,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             b0 = float(np.ravel(base)[0])
-            out["cpu_baseline"] = cpu_baseline(args.config, desc, percent, b0, args.seed,
+            out["cpu_baseline"] = cpu_baseline(args.config, w.desc, percent, b0, args.seed,
                                                seconds=args.cpu_seconds)
-            out["cpu_native_1core"] = native_cpu_rate(g, init, k, PROPOSALS[proposal], percent,
-                                                      b0, args.seed)
+            out["cpu_native"] = native_cpu_baseline(w, bounds, b0, args.seed,
+                                                    seconds=args.cpu_seconds)
         print(json.dumps(out), flush=True)
     ch.close()
     dg.close()

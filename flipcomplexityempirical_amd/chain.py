@@ -148,6 +148,10 @@ class Chains:
         self.n_chains, self.k = int(n_chains), int(k)
         self.mode = PROPOSALS[proposal] if isinstance(proposal, str) else int(proposal)
         lab = np.ascontiguousarray(init_labels, np.int16)
+        if lab.ndim == 2 and lab.shape[0] not in (1, n_chains):
+            raise ValueError(f"init_labels has {lab.shape[0]} rows: need 1 or n_chains={n_chains}")
+        if lab.ndim not in (1, 2) or lab.shape[-1] != g.n:
+            raise ValueError(f"init_labels must be [{g.n}] or [rows, {g.n}], got {lab.shape}")
         per_chain = 1 if lab.ndim == 2 and lab.shape[0] == n_chains and n_chains > 1 else 0
         if lab.ndim == 2 and not per_chain:
             lab = np.ascontiguousarray(lab[0])

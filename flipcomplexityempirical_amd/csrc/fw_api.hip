@@ -465,6 +465,11 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   FwRunParams& p = c->p;
   p.qcap = list_cap(256);
   p.qcap16 = list_cap(384);
+  {  // FLIPWALK_FOLD_AT=x: fold the attempt-driven 32-bit counters early (tests)
+    const char* e = getenv("FLIPWALK_FOLD_AT");
+    const long long v = e && e[0] ? atoll(e) : 0;
+    p.fold_at = v >= 64 && v <= 0x80000000ll ? (uint32_t)v : 0x80000000u;
+  }
   {  // FLIPWALK_NO_BITBOARD=1: the grid kernel runs every exact search as the list search
     const char* e = getenv("FLIPWALK_NO_BITBOARD");
     p.no_bb = e && e[0] == '1' ? 1 : 0;
@@ -587,14 +592,29 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
   if (steps == 0) return FW_OK;
   if (c->d_acc && c->max_yields + (uint64_t)steps + 1 >= 0xFFFFFFFFull)
     return fail(FW_EUNSUPPORTED, "spatial maps hold yield indices below 2^32");
+  if (c->p.trace && steps > FW_MAX_LAUNCH_STEPS)
+    return fail(FW_EUNSUPPORTED, "a traced run takes at most %lld steps", (long long)FW_MAX_LAUNCH_STEPS);
   c->max_yields += (uint64_t)steps + (c->ran ? 0 : 1);
   c->ran = true;
-  c->p.steps = steps;
   c->p.max_retries = max_retries;
-  HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  if (fw_launch_run(c->p, c->lb, c->grid, c->stream) != 0)
-    return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+  // the kernels count a launch's steps (and the per-step sums of degrees and boundary
+  // changes) in 32 bits: a longer run is a sequence of launches of at most
+  // FW_MAX_LAUNCH_STEPS counted steps (the trajectory does not depend on the split)
+  int64_t cap = FW_MAX_LAUNCH_STEPS;
+  {  // FLIPWALK_LAUNCH_STEPS=x: a smaller cap (tests of the split)
+    const char* e = getenv("FLIPWALK_LAUNCH_STEPS");
+    const long long v = e && e[0] ? atoll(e) : 0;
+    if (v >= 1 && v < cap) cap = v;
+  }
+  for (int64_t left = steps; left > 0;) {
+    const int64_t s = left < cap ? left : cap;
+    c->p.steps = s;
+    HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
+    if (fw_launch_run(c->p, c->lb, c->grid, c->stream) != 0)
+      return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    left -= s;
+  }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   return FW_OK;

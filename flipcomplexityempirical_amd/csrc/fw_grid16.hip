@@ -502,8 +502,13 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     };
     if (FULL && p.sched) sched_row(0);
     // attempts and yields of this launch in 32 bits: attempts = att0 + n_att, and every
-    // counted step is one yield (plus the initial state's on a chain's first launch)
-    const uint64_t att0 = stp->attempts;
+    // counted step is one yield (plus the initial state's on a chain's first launch).
+    // The counters that grow with attempts (n_att, n_popf, n_conf, n_sdeg) are folded
+    // into the 64-bit totals at a Philox refill once n_sdeg (the fastest: >= 2 per
+    // attempt) reaches p.fold_at (2^31; tests lower it), so no launch length wraps them; the host caps the counted
+    // steps of one launch (fw_chains_run_async), which bounds the rest.
+    uint64_t att0 = stp->attempts;
+    const bool first = has && !stp->stuck && stp->yields == 0 && att0 == 0;
     uint32_t n_att = 0;
     const uint64_t yields0 = stp->yields;
     int32_t stuck = has ? stp->stuck : 1;
@@ -575,7 +580,6 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       hb0 += ib == q;
       hb1 += ib == q + ROW;
     };
-    const bool first = has && !stuck && yields0 == 0 && att0 == 0;
     observe(first);
 
     // Philox batches: lane q of a row holds the draw of its chain's attempt (base + q).
@@ -594,6 +598,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (ballot(act) == 0ull) break;
 
       if (bpos == ROW) {
+        if (n_sdeg >= p.fold_at) {  // rare: fold (see att0); one row at a time
+          if (q == 0 && has) {
+            stp->pop_fail += n_popf;
+            stp->contig_fail += n_conf;
+            stp->sum_deg += n_sdeg;
+          }
+          att0 += n_att;
+          n_att = n_popf = n_conf = n_sdeg = 0;
+        }
         const uint64_t t = att0 + (uint64_t)(n_att + (uint32_t)q);
         pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
                     in_vgpr(key0), in_vgpr(key1));

@@ -11,6 +11,9 @@
 #define FW_MAX_DEG 63   // lanes 1..deg of one wave hold v's neighbours during commit
 #define FW_MAX_K 64     // foreign-label sets are 64-bit masks
 #define FW_HIST_PAD 64  // histogram window slack past the last bin
+// counted steps per kernel launch: per-launch step counters and the per-step sums of
+// degrees (<= 63) and boundary changes (<= 64) stay below 2^31 in 32 bits
+#define FW_MAX_LAUNCH_STEPS (1ll << 25)
 
 struct FwGraphDev {
   const int32_t* rowptr;  // [n+1]
@@ -54,6 +57,7 @@ struct FwRunParams {
   int64_t chain_id0;
   int64_t steps;
   int32_t max_retries;
+  uint32_t fold_at;             // n_sdeg at which attempt-driven 32-bit counters fold (2^31)
   int32_t qcap;                // search-list entries held in LDS
   // LDS layout (bytes from the dynamic shared base)
   int32_t lab_bytes;           // packed label bytes (multiple of 16)

@@ -163,6 +163,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           break;
         }
         if (bpos == WAVE) {
+          // the per-launch counters that grow with attempts fold into the 64-bit totals
+          // long before they can wrap (n_sdeg, the fastest, grows by <= 63 per attempt)
+          if (n_sdeg >= p.fold_at) {
+            if (lane == 0) {
+              stp->pop_fail += n_popf;
+              stp->contig_fail += n_conf;
+              stp->sum_deg += n_sdeg;
+            }
+            n_popf = n_conf = n_sdeg = 0;
+          }
           const uint64_t t = attempts + (uint64_t)lane;
           pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
                       in_vgpr(key0), in_vgpr(key1));

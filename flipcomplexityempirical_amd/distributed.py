@@ -56,18 +56,48 @@ def gather_stats(stats: np.ndarray, n_total: int, dist=None, lo: int = 0) -> np.
     return np.ascontiguousarray(merged).view(stats.dtype).reshape(n_total)
 
 
+def _local_device(device: Optional[int]) -> int:
+    """The GPU of this process: explicit, else LOCAL_RANK (one process per GPU per node)."""
+    if device is not None:
+        return int(device)
+    import os
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _shard_rows(x, n_total: int, lo: int, hi: int):
+    """Rows [lo, hi) of a per-chain array ([n_total, ...]); shared values pass through."""
+    if x is None or np.ndim(x) == 0:
+        return x
+    a = np.asarray(x)
+    if a.shape[0] == n_total and (a.ndim == 2 or (a.ndim == 1 and a.dtype.kind == "f")):
+        return a[lo:hi]
+    return a
+
+
 def run_sharded(graph, init_labels, k: int, n_total: int, steps: int, dist=None,
-                device: Optional[int] = None, **kw):
+                device: Optional[int] = None, engine=None, **kw):
     """Strong-scaling run: ``n_total`` chains split over the process group.
 
+    Rank r runs global chain ids ``shard_range(n_total, world, r)`` on its node-local GPU
+    (LOCAL_RANK unless ``device`` is given).  Per-chain inputs (``init_labels`` of shape
+    [n_total, n], ``base`` of length n_total) are sliced to the rank's rows; shared ones
+    are passed as they are.  ``engine`` (default ``chain.run_chains``, the GPU path) has
+    run_chains' signature; tests substitute a CPU engine to check the sharding alone.
     Returns (local RunResult, merged hist_cut, merged hist_b, merged stats[n_total]).
     """
     from .chain import run_chains
+    engine = engine or run_chains
     world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
     rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
     lo, hi = shard_range(n_total, world, rank)
-    res = run_chains(graph, init_labels, k, hi - lo, steps, chain_id0=lo,
-                     device=rank if device is None else device, **kw)
+    init = np.asarray(init_labels)
+    if init.ndim == 2 and init.shape[0] == n_total and n_total > 1:
+        init = init[lo:hi]
+    kw = dict(kw)
+    if "base" in kw:
+        kw["base"] = _shard_rows(kw["base"], n_total, lo, hi)
+    res = engine(graph, init, k, hi - lo, steps, chain_id0=lo, device=_local_device(device),
+                 **kw)
     hc, hb = merge_histograms(res.hist_cut, res.hist_b, dist)
     st = gather_stats(res.stats, n_total, dist, lo)
     return res, hc, hb, st

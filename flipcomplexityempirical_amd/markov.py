@@ -420,9 +420,14 @@ class MarkovChain:
             for code in tr:
                 if code < -1:
                     raise RuntimeError("chain stuck: no valid proposal within max_retries")
+                # GerryChain's MarkovChain erases the current state's parent link once the
+                # next proposal exists, so a yielded state's grandparent is None and the
+                # chain's history is not kept alive (a re-yielded state loses its parent)
+                prev = state
                 if code >= 0:
                     v, d = divmod(int(code), 64)
                     state = state.flip({nodes[v]: vals[d]})
+                prev.parent = None
                 yield state
             remaining -= s
         ch.close()

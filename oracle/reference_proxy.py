@@ -29,7 +29,7 @@ implementation of the chain semantics:
 * per-yield observables rce / rbn / waits (grid_chain_sec11.py:367-369)
 
 With the same seed it follows the same trajectory as oracle/flipchain_oracle.c and
-the HIP path (tests/test_proxy.py checks this).
+the HIP path (tests/test_oracle.py::test_proxy_follows_the_same_trajectory checks this).
 """
 from __future__ import annotations
 

@@ -85,3 +85,69 @@ def test_merge_without_process_group_is_identity():
     a, b = np.arange(5, dtype=np.uint64), np.arange(3, dtype=np.uint64)
     x, y = merge_histograms(a, b, None)
     assert x is a and y is b
+
+
+def oracle_engine(graph, init_labels, k, n_chains, steps, chain_id0=0, device=0, proposal="pairs",
+                  pop_bounds=None, base=1.0, seed=0, **_):
+    """run_chains' signature and result on the CPU oracle (test stand-in for the GPU)."""
+    from flipcomplexityempirical_amd.chain import (PROPOSALS, RunResult, metropolis_table)
+    from oracle import oracle as O
+    hc = np.zeros(graph.n_edges + 1, np.uint64)
+    hb = np.zeros(graph.n + 1, np.uint64)
+    st = np.zeros(n_chains, O.STATS_DTYPE)
+    init = np.asarray(init_labels)
+    bases = np.broadcast_to(np.asarray(base, np.float64), (n_chains,))
+    labs = []
+    for i in range(n_chains):
+        lab0 = init[i] if init.ndim == 2 else init
+        lab, s, _, _ = O.run_chain(graph, lab0, k, PROPOSALS[proposal], *pop_bounds,
+                                   metropolis_table(bases[i], graph.maxdeg), seed, chain_id0 + i,
+                                   steps, hist_cut=hc, hist_b=hb)
+        st[i] = s[0]
+        labs.append(lab)
+    return RunResult(np.stack(labs), st, hc, hb, None, 0.0)
+
+
+def _sharded_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from test_distributed import _sharded_inputs, oracle_engine
+    from flipcomplexityempirical_amd.distributed import run_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g, init, bases, bounds = _sharded_inputs()
+    res, hc, hb, st = run_sharded(g, init, 4, N_TOTAL, STEPS, dist, engine=oracle_engine,
+                                  proposal="pairs", pop_bounds=bounds, base=bases, seed=SEED)
+    lo, hi = shard_range(N_TOTAL, world, rank)
+    assert len(res.stats) == hi - lo
+    if rank == 0:
+        np.savez(out, hc=hc, hb=hb, st=st.view(np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _sharded_inputs():
+    from flipcomplexityempirical_amd.chain import population_bounds
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    g = grid_graph(12, 12)
+    init = np.stack([block_seed(12, 12, 2, 2)] * N_TOTAL)
+    init[N_TOTAL // 2:] = np.ascontiguousarray(
+        block_seed(12, 12, 2, 2).reshape(12, 12).T).reshape(-1)  # per-chain plans differ
+    bases = np.geomspace(0.5, 2.0, N_TOTAL)  # per-chain bases
+    return g, init, bases, population_bounds(g.n, 4, 0.10)
+
+
+def test_run_sharded_two_ranks_slices_per_chain_inputs(tmp_path):
+    """run_sharded over gloo, world 2: each rank runs its id range with ITS rows of the
+    per-chain plans and bases; the merged result equals one process running all chains."""
+    out = str(tmp_path / "sharded.npz")
+    mp.start_processes(_sharded_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    g, init, bases, bounds = _sharded_inputs()
+    ref = oracle_engine(g, init, 4, N_TOTAL, STEPS, proposal="pairs", pop_bounds=bounds,
+                        base=bases, seed=SEED)
+    assert np.array_equal(got["hc"], ref.hist_cut) and np.array_equal(got["hb"], ref.hist_b)
+    assert np.array_equal(got["st"], ref.stats.view(np.uint8))

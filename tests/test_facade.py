@@ -64,8 +64,17 @@ def test_reference_script_shape_runs_on_gpu(gpu_lib):
     chain = gc.MarkovChain(gc.slow_reversible_propose_bi,
                            gc.Validator([gc.single_flip_contiguous, pb]), accept=gc.cut_accept,
                            initial_state=part, total_steps=1500, seed=5, chain_id=3, chunk=600)
-    parts = list(chain)
+    parts, child_ok = [], None
+    for p in chain:
+        if p.parent is not None:
+            # GerryChain erases the parent of the previous state: history is not kept alive
+            assert p.parent.parent is None
+            if child_ok is None:  # single_flip_contiguous on a child, while its parent lives
+                child_ok = gc.single_flip_contiguous(p)
+        parts.append(p)
     assert len(parts) == 1500 and parts[0] is part
+    assert child_ok is True
+    assert sum(p.parent is not None for p in parts[:-1]) == 0
     # the reference re-yields the same object after a Metropolis rejection
     assert any(a is b for a, b in zip(parts, parts[1:]))
     lo, hi = population_bounds(g.n, 2, 0.05)
@@ -75,9 +84,6 @@ def test_reference_script_shape_runs_on_gpu(gpu_lib):
     # the per-yield observables of grid_chain_sec11.py:367-369 agree with the oracle's sums
     assert sum(len(p["cut_edges"]) for p in parts) == int(ost["sum_cut"][0])
     assert sum(len(p["b_nodes"]) for p in parts) == int(ost["sum_bnodes"][0])
-    # single_flip_contiguous on a yielded child agrees (evaluated by the GPU eval kernel)
-    child = next(p for p in parts[1:] if p.parent is not None)
-    assert gc.single_flip_contiguous(child) is True
 
 
 @pytest.mark.gpu

@@ -355,3 +355,31 @@ def test_bitboard_window_escape(gpu_lib, k, vertical, path, monkeypatch):
         for f in ("attempts", "steps", "accepts", "contig_fail", "bfs_runs", "bfs_nodes", "bfs_deg"):
             assert int(st[f][i]) == int(ost[f][0]), (i, f, st[f][i], ost[f][0])
     assert (st["bfs_nodes"] > 40 * st["bfs_runs"]).any()  # searches far past the window
+
+
+@pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
+                                       ("sec11_a2_k2", "auto"), ("tract_k4", "auto")])
+def test_counter_fold_bit_exact(gpu_lib, name, path, monkeypatch):
+    """The 32-bit per-launch counters that grow with attempts (attempts, population and
+    contiguity failures, summed proposal degrees) fold into the 64-bit totals at a Philox
+    refill; FLIPWALK_FOLD_AT=64 folds every few refills instead of at 2^31.  Totals and
+    trajectories must not change."""
+    monkeypatch.setenv("FLIPWALK_FOLD_AT", "64")
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    st = _run_vs_oracle(case, 13, [500, 700])
+    assert (st["sum_deg"] > 20 * 64).all()  # many folds happened
+
+
+@pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("sec11_a2_k2", "auto")])
+def test_long_run_split_into_launches(gpu_lib, name, path, monkeypatch):
+    """fw_chains_run splits a run into launches of at most FW_MAX_LAUNCH_STEPS counted steps
+    (the kernels' per-launch 32-bit step counters); FLIPWALK_LAUNCH_STEPS=97 forces many
+    launches per call.  Trajectories and totals equal one oracle run."""
+    monkeypatch.setenv("FLIPWALK_LAUNCH_STEPS", "97")
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    _run_vs_oracle(case, 11, [1000, 333])

@@ -193,3 +193,133 @@ def test_c2_time_averaged_histograms_batch_means(gpu_lib):
         assert np.abs(z).max() < 5.0, (f, np.abs(z).max())
         chi2 = float((z ** 2).sum())
         assert sps.chi2.sf(chi2, int(live.sum())) > 1e-3, (f, chi2, int(live.sum()))
+
+
+def _full_size_properties(g, k, bounds, init, labs, st, hc, hb, pops, sample, steps_total):
+    """Size-independent checks of a batched run: counters, histogram moments, and the
+    recomputed cut / boundary / populations / contiguity of a sample of final plans."""
+    assert (st["steps"] == steps_total).all() and (st["yields"] == steps_total + 1).all()
+    assert not st["stuck"].any()
+    assert (st["attempts"] == st["steps"] + st["pop_fail"] + st["contig_fail"]).all()
+    assert hc.sum() == hb.sum() == st["yields"].sum()
+    assert int((hc * np.arange(len(hc), dtype=np.uint64)).sum()) == int(st["sum_cut"].sum())
+    assert int((hb * np.arange(len(hb), dtype=np.uint64)).sum()) == int(st["sum_bnodes"].sum())
+    total = int(g.total_pop)
+    assert (pops.sum(1) == total).all() and (pops >= bounds[0]).all() and (pops <= bounds[1]).all()
+    e = g.edges()
+    w = g.pop_array()
+    for i in sample:
+        lab = labs[i]
+        m = lab[e[:, 0]] != lab[e[:, 1]]
+        assert int(m.sum()) == st["cut"][i]
+        assert len(np.unique(e[m].ravel())) == st["bnodes"][i]
+        assert np.array_equal(np.bincount(lab, weights=w, minlength=k).astype(np.int64), pops[i])
+        assert O.plan_valid(g, lab, k, *bounds)
+
+
+def _oracle_rerun(g, init, k, mode, bounds, thr, seed, cid, steps_list):
+    olab, ost = init.copy(), O.new_stats(1)
+    for s in steps_list:
+        olab, ost, _, _ = O.run_chain(g, olab, k, mode, *bounds, thr, seed, int(cid), s, stats=ost)
+    return olab, ost
+
+
+def test_c4_full_size_properties(gpu_lib):
+    """BASELINE configs[3] at its stated size: the 9,000-node Delaunay dual graph, k=18 tree
+    seed, 16,384 chains, with the production LDS plan the host picks for it (160-entry
+    visit list + HBM spill, 16 chains per CU; no FLIPWALK_* overrides)."""
+    from flipcomplexityempirical_amd.workloads import workload
+    for var in ("FLIPWALK_LIST_CAP", "FLIPWALK_NO_BITBOARD", "FLIPWALK_NO_GRID16"):
+        assert var not in os.environ
+    w = workload("c4")
+    g, init, k = w.graph, w.init, w.k
+    C, S, seed = w.chains, 250, 3
+    bounds = population_bounds(g.total_pop, k, w.percent)
+    dg = DeviceGraph(g)
+    assert dg.n == 9000 and dg.grid_w == 0
+    ch = Chains(dg, C, k, init, proposal=w.proposal, pop_bounds=bounds, base=w.base, seed=seed)
+    ch.run(S)
+    ch.run(S)
+    st, hc, hb, pops, labs = ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(), ch.labels()
+    rng = np.random.default_rng(4)
+    sample = np.unique(np.concatenate([rng.integers(0, C, 200), [0, 1, C - 2, C - 1]]))
+    _full_size_properties(g, k, bounds, init, labs, st, hc, hb, pops, sample, 2 * S)
+    assert st["bfs_runs"].sum() > 0 and st["contig_fail"].sum() > 0
+    thr = metropolis_table(w.base, g.maxdeg)
+    for i in sample[::12]:  # full-size bit-exact re-runs on the oracle
+        olab, ost = _oracle_rerun(g, init, k, 1, bounds, thr, seed, i, [S, S])
+        assert np.array_equal(olab, labs[i]), i
+        for f in ("attempts", "steps", "accepts", "contig_fail", "bfs_runs", "bfs_nodes",
+                  "bfs_deg", "sum_cut", "sum_bnodes", "cut", "bnodes", "npairs"):
+            assert ost[f][0] == st[f][i], (i, f)
+        assert ost["sum_invb"][0] == st["sum_invb"][i]
+
+
+def test_c5_ladder_shard_full_size_properties(gpu_lib):
+    """BASELINE configs[4], one GPU's shard at 8 GPUs: global chain ids [0, 8192) of the
+    200x200 k=8 workload = 8 whole 1,024-chain base groups of the 64-base ladder (per-chain
+    Metropolis tables), run in one handle."""
+    from flipcomplexityempirical_amd.distributed import shard_range
+    from flipcomplexityempirical_amd.workloads import ladder, ladder_base_index, workload
+    w = workload("c5")
+    g, init, k = w.graph, w.init, w.k
+    lo, hi = shard_range(w.chains, 8, 0)
+    assert (lo, hi) == (0, 8192)
+    bases = w.bases(lo, hi)
+    assert len(np.unique(bases)) == 8 and np.unique(ladder_base_index(np.arange(lo, hi))).size == 8
+    C, S, seed = hi - lo, 150, 21
+    bounds = population_bounds(g.total_pop, k, w.percent)
+    dg = DeviceGraph(g)
+    ch = Chains(dg, C, k, init, proposal=w.proposal, pop_bounds=bounds, base=bases, seed=seed,
+                chain_id0=lo)
+    ch.run(S)
+    ch.run(S)
+    st, hc, hb, pops, labs = ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(), ch.labels()
+    rng = np.random.default_rng(5)
+    sample = np.unique(np.concatenate([rng.integers(0, C, 120), [0, 1023, 1024, C - 1]]))
+    _full_size_properties(g, k, bounds, init, labs, st, hc, hb, pops, sample, 2 * S)
+    for i in sample[::10]:
+        thr = metropolis_table(float(bases[i]), g.maxdeg)
+        olab, ost = _oracle_rerun(g, init, k, 1, bounds, thr, seed, lo + i, [S, S])
+        assert np.array_equal(olab, labs[i]), i
+        for f in ("attempts", "steps", "accepts", "contig_fail", "bfs_runs", "bfs_nodes",
+                  "sum_cut", "sum_bnodes", "cut", "bnodes", "npairs"):
+            assert ost[f][0] == st[f][i], (i, f)
+        assert ost["sum_invb"][0] == st["sum_invb"][i]
+    # low ladder bases favour long boundaries (base < 1), high ones short ones
+    lad = ladder()[ladder_base_index(np.arange(lo, hi))]
+    assert st["cut"][lad < 0.5].mean() > st["cut"][lad > 2.0].mean()
+
+
+def test_rccl_histogram_merge_on_device(gpu_lib):
+    """The one collective of the multi-GPU path, on RCCL: a 1-rank "nccl" process group
+    merges histograms and per-chain stats held as device tensors (distributed.py)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from flipcomplexityempirical_amd.distributed import gather_stats, merge_histograms
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        assert dist.get_backend() == "nccl"
+        g = grid_graph(20, 20)
+        init = block_seed(20, 20, 2, 2)
+        bounds = population_bounds(g.total_pop, 4, 0.05)
+        ch = Chains(DeviceGraph(g), 64, 4, init, proposal="pairs", pop_bounds=bounds, base=MU,
+                    seed=1)
+        ch.run(200)
+        hc, hb = ch.hist_cut(), ch.hist_b()
+        mhc, mhb = merge_histograms(hc, hb, dist)
+        assert np.array_equal(mhc, hc) and np.array_equal(mhb, hb)
+        st = ch.stats()
+        mst = gather_stats(st, 64, dist, 0)
+        assert mst.tobytes() == st.tobytes()
+    finally:
+        dist.destroy_process_group()

@@ -41,6 +41,7 @@ def _ours(base, runs):
     (MU, 263, [(a, p) for a in (0, 1, 2) for p in POPS]),
     (10.0, 1000, [(a, p) for a in (0, 1, 2) for p in POPS]),
     (1.0, 100, [(0, 0.05), (1, 0.5), (2, 0.9), (0, 0.9)]),
+    (0.1, 10, [(a, p) for a in (0, 1, 2) for p in POPS]),
 ])
 def test_sec11_mean_wait_matches_reference(base, label, runs):
     ref = json.load(open(os.path.join(GOLDEN, "wait_sec11.json")))
@@ -88,3 +89,56 @@ def test_frankengraph_mean_wait_matches_reference(label):
     se = np.sqrt(s2 * (1 / 3 + 1 / 3))
     for a, (o, r) in groups.items():
         assert abs(o.mean() - r.mean()) < 3 * se, (a, o, r, se)
+
+
+# All_States_Chain.py:36-38: bases and population tolerances of the Kansas runs
+KS_BASES = {10: .1, 14: 1 / MU ** 2, 20: .2, 37: 1 / MU, 80: .8, 100: 1.0}
+KS_POPS = {5: .05, 10: .1, 50: .5, 90: .9}
+KS_UNITS = {"BG": "BG20", "COUSUB": "COUSUB20", "Tract": "Tract20", "County": "County20"}
+
+
+def _ks_ours(unit, base_label, T):
+    """The oracle on one (unit, base) cell of All_States_Chain.py: k=2 on the Kansas dual
+    graph, slow_reversible_propose_bi, cut_accept, T yields, a fresh recursive_tree_part
+    seed (epsilon .05, :232) per run as the reference draws one per run; mean wait per
+    yield of each of the four population tolerances."""
+    from cases import kansas
+    from flipcomplexityempirical_amd.seeds import recursive_tree_part
+    g = kansas(KS_UNITS[unit])
+    M = float(g.n ** 2 - 1)
+    b = KS_BASES[base_label]
+    out = []
+    for pl, p in KS_POPS.items():
+        lab = recursive_tree_part(g, [0, 1], g.total_pop / 2, 0.05, seed=1000 * base_label + pl)
+        lo, hi = population_bounds(g.total_pop, 2, p)
+        _, st, _, _ = O.run_chain(g, lab, 2, 0, lo, hi, metropolis_table(b, g.maxdeg), 7,
+                                  100 * base_label + pl, T - 1)
+        out.append((M * st["sum_invb"][0] - st["yields"][0]) / T)
+    return np.array(out)
+
+
+@pytest.mark.parametrize("key,T", [("States20", 10000), ("KS2", 100000)])
+def test_kansas_mean_wait_matches_reference(key, T):
+    """plots/States/20/*wait.txt (All_States_Chain.py with fips 20: Kansas BG / COUSUB /
+    Tract / County dual graphs, k=2, total_steps 10,000) and plots/KS2/*wait.txt (the same
+    chain at 100,000 yields): for every unit and every base <= 1 (short burn-in; the
+    reference's seed plan is a random tree partition, ours another draw of the same
+    procedure), the oracle's mean wait per yield over the four population tolerances
+    against the reference's four runs.  Each of the 24 cells within 3.5 combined standard
+    errors (4 + 4 runs), and the mean squared z within what two 4-run samples give
+    (t-tails: E[z^2] ~ 1.5).  Fixture: tests/golden/wait_ks.json."""
+    from concurrent.futures import ThreadPoolExecutor
+    ref = json.load(open(os.path.join(GOLDEN, "wait_ks.json")))[key]
+    cells = [(u, bl) for u in KS_UNITS for bl in KS_BASES]
+    # ctypes releases the GIL: the oracle chains of the cells run on a thread pool
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        ours = list(ex.map(lambda c: _ks_ours(c[0], c[1], T), cells))
+    zs = []
+    for (u, bl), o in zip(cells, ours):
+        r = np.array([x["wait_sum"] / T for x in ref if x["unit"] == u and x["base_label"] == bl])
+        assert len(r) == 4
+        se = np.sqrt(r.var(ddof=1) / len(r) + o.var(ddof=1) / len(o))
+        z = (o.mean() - r.mean()) / se
+        zs.append(z)
+        assert abs(z) < 3.5, (key, u, bl, o.mean(), r.mean(), se)
+    assert float(np.mean(np.square(zs))) < 2.5, (key, zs)
