@@ -243,6 +243,77 @@ class Chains:
         self._sched = r
         check(_lib.load().fw_chains_set_schedule(self._h, ptr(r), r.shape[0], int(t0)))
 
+    # ------------------------------------------------------------- district shapes
+    def enable_ring(self, ring_u, ring_w) -> None:
+        """Count yields per pair of first two cut ring edges (boundary_slope and the
+        driver's slope / angle, grid_chain_sec11.py:55-78,371-394); ``shape.ring_edges``
+        builds the ring of a graph from the reference's predicates.  Zeroes the histogram."""
+        u = np.ascontiguousarray(ring_u, np.int32)
+        w = np.ascontiguousarray(ring_w, np.int32)
+        if u.shape != w.shape or u.ndim != 1:
+            raise ValueError("ring_u and ring_w must be equal-length 1-D arrays")
+        check(_lib.load().fw_chains_enable_ring(self._h, ptr(u), ptr(w), len(u)))
+        self.ring = (u, w)
+
+    def hist_ring(self) -> np.ndarray:
+        """uint64 [R*R+1]: yields per ring pair (i*R + j, i < j); [R*R]: fewer than two."""
+        R = len(self.ring[0])
+        return self._read(_lib.READ_HIST_RING, np.empty(R * R + 1, np.uint64))
+
+    def ring_pairs(self) -> np.ndarray:
+        """int32 [n_chains, 2]: each chain's current first two cut ring edges (-1: none)."""
+        return self._read(_lib.READ_RING_PAIR, np.empty((self.n_chains, 2), np.int32))
+
+    # ------------------------------------------------------------- checkpoint / resume
+    def checkpoint(self) -> dict:
+        """Everything a resumed chain needs: plans, the stats records (with the Philox
+        attempt counter: the counter-based RNG makes resume exact) and the histograms."""
+        ck = {"labels": self.labels(), "stats": self.stats(), "hist_cut": self.hist_cut(),
+              "hist_b": self.hist_b(), "seed": np.uint64(self.seed),
+              "chain_id0": np.int64(self.chain_id0), "thr": self.thr}
+        if getattr(self, "ring", None) is not None:
+            ck["hist_ring"] = self.hist_ring()
+            ck["ring_u"], ck["ring_w"] = self.ring
+        return ck
+
+    def restore(self, ck: dict) -> None:
+        """Load a ``checkpoint`` into this handle (same graph, chain count, seed and chain
+        ids): the chains continue exactly where the checkpointed ones stopped."""
+        if int(ck["seed"]) != self.seed or int(ck["chain_id0"]) != self.chain_id0:
+            raise ValueError("checkpoint of another seed / chain-id range")
+        L = _lib.load()
+        for what, key in ((_lib.READ_LABELS, "labels"), (_lib.READ_STATS, "stats"),
+                          (_lib.READ_HIST_CUT, "hist_cut"), (_lib.READ_HIST_B, "hist_b")):
+            a = np.ascontiguousarray(ck[key])
+            if key == "stats":
+                a = np.ascontiguousarray(a, STATS_DTYPE)
+                if a.shape != (self.n_chains,):
+                    raise ValueError("checkpoint of another chain count")
+            check(L.fw_chains_write(self._h, what, ptr(a), a.nbytes))
+        if "hist_ring" in ck:
+            self.enable_ring(ck["ring_u"], ck["ring_w"])
+            a = np.ascontiguousarray(ck["hist_ring"], np.uint64)
+            check(L.fw_chains_write(self._h, _lib.READ_HIST_RING, ptr(a), a.nbytes))
+
+    def save_checkpoint(self, path: str) -> None:
+        ck = self.checkpoint()
+        ck["stats"] = ck["stats"].view(np.uint8)  # plain bytes: loadable without pickle
+        np.savez(path, **ck)
+
+    @classmethod
+    def from_checkpoint(cls, dgraph: "DeviceGraph", path: str, k: int, proposal="pairs",
+                        pop_bounds=None, percent: float = 0.05) -> "Chains":
+        """A new handle resumed from ``save_checkpoint`` output (numpy, no pickle)."""
+        d = np.load(path, allow_pickle=False)
+        labels = d["labels"]
+        ch = cls(dgraph, labels.shape[0], k, labels, proposal=proposal, pop_bounds=pop_bounds,
+                 percent=percent, seed=int(d["seed"]), chain_id0=int(d["chain_id0"]),
+                 thr=d["thr"])
+        ck = {key: d[key] for key in d.files}
+        ck["stats"] = d["stats"].view(STATS_DTYPE)
+        ch.restore(ck)
+        return ch
+
     # ------------------------------------------------------------- spatial maps
     def enable_maps(self, label_values: Optional[Sequence[int]] = None) -> None:
         """Track the reference driver's per-edge / per-node maps on every chain

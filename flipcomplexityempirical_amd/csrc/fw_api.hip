@@ -162,6 +162,12 @@ struct fw_chains {
   // fw_chains_set_schedule
   double* d_sched = nullptr;
   uint64_t* d_sched53 = nullptr;
+  // fw_chains_enable_ring
+  int32_t ring_n = 0;
+  std::vector<int32_t> ring_u, ring_w;
+  int32_t* d_ring = nullptr;              // [2][ring_n] endpoints
+  uint8_t* d_ring_node = nullptr;         // [n]
+  unsigned long long* d_hist_ring = nullptr;  // [ring_n^2 + 1]
 };
 
 namespace {
@@ -244,13 +250,24 @@ bool plan_valid(const fw_graph* g, const int16_t* lab, int k, int64_t lo, int64_
   return true;
 }
 
+size_t ring_bins(int r) { return (size_t)r * (size_t)r + 1; }
+
+// first two cut ring edges of a plan in ring order: out = {i, j} (-1, -1 if fewer than two)
+void ring_pair_of(const fw_chains* c, const int16_t* lab, int32_t* out) {
+  out[0] = out[1] = -1;
+  int found = 0;
+  for (int r = 0; r < c->ring_n && found < 2; ++r)
+    if (lab[c->ring_u[r]] != lab[c->ring_w[r]]) out[found++] = r;
+  if (found < 2) out[0] = out[1] = -1;
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* fw_last_error(void) { return g_err.c_str(); }
 
-int32_t fw_version(void) { return 0x000300; }
+int32_t fw_version(void) { return 0x000400; }
 
 int32_t fw_device_count(void) {
   int c = 0;
@@ -418,7 +435,8 @@ void fw_chains_destroy(fw_chains* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_thr53, c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
-                  c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt, c->d_sched, c->d_sched53};
+                  c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt, c->d_sched, c->d_sched53,
+                  c->d_ring,   c->d_ring_node, c->d_hist_ring};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -477,7 +495,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   // +8: the grid kernels read label dwords one past the last node
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
   p.off_gsum = p.lab_bytes;
-  p.off_list = p.off_gsum + round16((int64_t)G * 4);
+  p.off_list = p.off_gsum + round16((int64_t)fw_run_gsum_words(G) * 4);
   p.lds_bytes = p.off_list + p.qcap * 4;
   if (G > 64 * 16) {
     delete c;
@@ -699,8 +717,81 @@ int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes) {
       if (bytes < need) return fail(FW_EINVAL, "pops need %zu bytes", need);
       HIPCHK(hipMemcpy(host_dst, c->d_pops, need, hipMemcpyDeviceToHost));
       return FW_OK;
+    case FW_READ_HIST_RING:
+      if (!c->ring_n) return fail(FW_ESTATE, "the ring observable is not enabled");
+      need = sizeof(uint64_t) * ring_bins(c->ring_n);
+      if (bytes < need) return fail(FW_EINVAL, "hist_ring needs %zu bytes", need);
+      HIPCHK(hipMemcpy(host_dst, c->d_hist_ring, need, hipMemcpyDeviceToHost));
+      return FW_OK;
+    case FW_READ_RING_PAIR: {
+      if (!c->ring_n) return fail(FW_ESTATE, "the ring observable is not enabled");
+      need = sizeof(int32_t) * 2 * (size_t)c->n_chains;
+      if (bytes < need) return fail(FW_EINVAL, "ring pairs need %zu bytes", need);
+      std::vector<uint8_t> packed((size_t)c->n_chains * c->p.lab_stride);
+      HIPCHK(hipMemcpy(packed.data(), c->d_labels, packed.size(), hipMemcpyDeviceToHost));
+      std::vector<int16_t> lab(n);
+      int32_t* out = static_cast<int32_t*>(host_dst);
+      for (int i = 0; i < c->n_chains; ++i) {
+        unpack_labels(packed.data() + (size_t)i * c->p.lab_stride, n, c->lb, lab.data());
+        ring_pair_of(c, lab.data(), out + 2 * (size_t)i);
+      }
+      return FW_OK;
+    }
     default:
       return fail(FW_EINVAL, "unknown read kind %d", what);
+  }
+}
+
+int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t bytes) {
+  if (!c || !host_src) return fail(FW_EINVAL, "fw_chains_write: null");
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int n = c->g->n;
+  size_t need = 0;
+  switch (what) {
+    case FW_READ_LABELS: {
+      need = sizeof(int16_t) * (size_t)c->n_chains * n;
+      if (bytes < need) return fail(FW_EINVAL, "labels need %zu bytes", need);
+      const int16_t* lab = static_cast<const int16_t*>(host_src);
+      std::vector<uint8_t> packed((size_t)c->n_chains * c->p.lab_stride);
+      std::vector<int64_t> pops((size_t)c->n_chains * c->k);
+      for (int i = 0; i < c->n_chains; ++i) {
+        std::string why;
+        if (!plan_valid(c->g, lab + (size_t)i * n, c->k, c->p.pop_lo, c->p.pop_hi,
+                        pops.data() + (size_t)i * c->k, &why))
+          return fail(FW_ESTATE, "plan %d invalid: %s", i, why.c_str());
+        pack_labels(lab + (size_t)i * n, n, c->lb, packed.data() + (size_t)i * c->p.lab_stride,
+                    c->p.lab_stride);
+      }
+      HIPCHK(hipMemcpy(c->d_labels, packed.data(), packed.size(), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(c->d_pops, pops.data(), sizeof(int64_t) * pops.size(),
+                       hipMemcpyHostToDevice));
+      return FW_OK;
+    }
+    case FW_READ_STATS:
+      need = sizeof(fw_chain_stats) * c->n_chains;
+      if (bytes < need) return fail(FW_EINVAL, "stats need %zu bytes", need);
+      HIPCHK(hipMemcpy(c->d_stats, host_src, need, hipMemcpyHostToDevice));
+      c->ran = true;  // the initial state was yielded in the run being resumed
+      return FW_OK;
+    case FW_READ_HIST_CUT:
+      need = sizeof(uint64_t) * (c->g->nnz / 2 + 1);
+      if (bytes < need) return fail(FW_EINVAL, "hist_cut needs %zu bytes", need);
+      HIPCHK(hipMemcpy(c->d_hist_cut, host_src, need, hipMemcpyHostToDevice));
+      return FW_OK;
+    case FW_READ_HIST_B:
+      need = sizeof(uint64_t) * (n + 1);
+      if (bytes < need) return fail(FW_EINVAL, "hist_b needs %zu bytes", need);
+      HIPCHK(hipMemcpy(c->d_hist_b, host_src, need, hipMemcpyHostToDevice));
+      return FW_OK;
+    case FW_READ_HIST_RING:
+      if (!c->ring_n) return fail(FW_ESTATE, "the ring observable is not enabled");
+      need = sizeof(uint64_t) * ring_bins(c->ring_n);
+      if (bytes < need) return fail(FW_EINVAL, "hist_ring needs %zu bytes", need);
+      HIPCHK(hipMemcpy(c->d_hist_ring, host_src, need, hipMemcpyHostToDevice));
+      return FW_OK;
+    default:
+      return fail(FW_EINVAL, "fw_chains_write: unsupported kind %d", what);
   }
 }
 
@@ -722,6 +813,8 @@ int fw_chains_reset_observables(fw_chains* c) {
   HIPCHK(hipMemset(c->d_hist_cut, 0,
                    sizeof(unsigned long long) * (c->g->nnz / 2 + 1 + FW_HIST_PAD)));
   HIPCHK(hipMemset(c->d_hist_b, 0, sizeof(unsigned long long) * (c->g->n + 1 + FW_HIST_PAD)));
+  if (c->d_hist_ring)
+    HIPCHK(hipMemset(c->d_hist_ring, 0, sizeof(unsigned long long) * ring_bins(c->ring_n)));
   if (c->d_acc) {  // maps restart from the current plans (yield indices restart at 0)
     const size_t C = (size_t)c->n_chains, n = (size_t)c->g->n, E = (size_t)c->g->nnz / 2;
     HIPCHK(hipMemset(c->d_acc, 0, sizeof(int64_t) * std::max<size_t>(C * E, 1)));
@@ -832,6 +925,45 @@ int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values) {
   if (fw_launch_map_init(p, c->stream) != 0)
     return fail(FW_EHIP, "map init launch failed: %s", hipGetErrorString(hipGetLastError()));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return FW_OK;
+}
+
+int fw_chains_enable_ring(fw_chains* c, const int32_t* ring_u, const int32_t* ring_w,
+                          int32_t n_ring) {
+  if (!c || !ring_u || !ring_w) return fail(FW_EINVAL, "fw_chains_enable_ring: null");
+  if (n_ring < 2 || n_ring > 1024) return fail(FW_EINVAL, "n_ring = %d outside [2, 1024]", n_ring);
+  const fw_graph* g = c->g;
+  std::vector<uint8_t> node((size_t)g->n, 0);
+  for (int r = 0; r < n_ring; ++r) {
+    const int u = ring_u[r], w = ring_w[r];
+    if (u < 0 || u >= g->n || w < 0 || w >= g->n ||
+        !std::binary_search(g->col.begin() + g->rowptr[u], g->col.begin() + g->rowptr[u + 1], w))
+      return fail(FW_EINVAL, "ring edge %d (%d, %d) is not an edge of the graph", r, u, w);
+    node[u] = node[w] = 1;
+  }
+  HIPCHK(hipSetDevice(g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->d_ring) (void)hipFree(c->d_ring);
+  if (c->d_hist_ring) (void)hipFree(c->d_hist_ring);
+  c->d_ring = nullptr;
+  c->d_hist_ring = nullptr;
+  if (!c->d_ring_node && hipMalloc(&c->d_ring_node, (size_t)g->n) != hipSuccess)
+    return fail(FW_ENOMEM, "ring node flags");
+  if (hipMalloc(&c->d_ring, sizeof(int32_t) * 2 * (size_t)n_ring) != hipSuccess ||
+      hipMalloc(&c->d_hist_ring, sizeof(unsigned long long) * ring_bins(n_ring)) != hipSuccess)
+    return fail(FW_ENOMEM, "ring histogram of %d edges", n_ring);
+  c->ring_u.assign(ring_u, ring_u + n_ring);
+  c->ring_w.assign(ring_w, ring_w + n_ring);
+  c->ring_n = n_ring;
+  HIPCHK(hipMemcpy(c->d_ring, ring_u, sizeof(int32_t) * n_ring, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_ring + n_ring, ring_w, sizeof(int32_t) * n_ring, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_ring_node, node.data(), node.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(c->d_hist_ring, 0, sizeof(unsigned long long) * ring_bins(n_ring)));
+  c->p.ring_n = n_ring;
+  c->p.ring_u = c->d_ring;
+  c->p.ring_w = c->d_ring + n_ring;
+  c->p.ring_node = c->d_ring_node;
+  c->p.hist_ring = c->d_hist_ring;
   return FW_OK;
 }
 

@@ -444,6 +444,15 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
   return verdict;
 }
 
+// Level-1 group sums of the one-chain-per-wave kernel: lane l owns groups l*PER .. l*PER +
+// PER-1, stored at l*(PER+1) + t.  The pad word per lane makes the PER per-lane reads of a
+// select conflict-free (lane stride PER+1 is odd: 32 distinct banks per 32-lane group;
+// without it, stride 16 put the 32 lanes of a ds_read_b32 group on 2 banks).
+template <int PER>
+__device__ __forceinline__ int gsum_slot(int g) {
+  return (g / PER) * (PER + 1) + (g % PER);
+}
+
 // E16: a general graph of max degree <= 16 whose adjacency rows are read from the padded
 // 16-wide table (four 16-byte loads in flight together) instead of walking CSR entries.
 template <int LB, bool GRID, bool E16 = false>
@@ -663,9 +672,10 @@ struct Ctx {
     uint32_t gs[PER];
     uint32_t s = 0;
     const int g0 = lane * PER;
+    const int slot_last = gsum_slot<PER>(G - 1);
 #pragma unroll
     for (int t = 0; t < PER; ++t) {  // unconditional (clamped) reads, masked values
-      const uint32_t w = gsum[min(g0 + t, G - 1)];
+      const uint32_t w = gsum[min(lane * (PER + 1) + t, slot_last)];
       gs[t] = g0 + t < G ? w : 0u;
       s += gs[t];
     }

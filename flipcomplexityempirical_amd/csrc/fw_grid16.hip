@@ -551,11 +551,34 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     lds_order();
     double invb = p.g.invb[bnodes];  // 1/|B| from the graph's table, no fp64 divide
 
+    // district-shape observable (FULL only): the pair of the first two cut ring edges in
+    // ring order, per row, counted per yield in runs flushed when it changes (a flip of a
+    // ring node) and at the end of the launch
+    const int RN = FULL ? p.ring_n : 0;
+    auto ring_pair = [&]() -> int32_t {  // row-uniform; called by whole rows
+      int f = -1, sc = -1;
+      for (int b0 = 0; b0 < RN; b0 += ROW) {
+        const int r = b0 + q;
+        const int ri = r < RN ? r : 0;
+        uint32_t m = rowbits(ballot(r < RN && P::get(lab, p.ring_u[ri]) != P::get(lab, p.ring_w[ri])),
+                             row);
+        if (m && f < 0) {
+          f = b0 + __ffs(m) - 1;
+          m &= m - 1;
+        }
+        if (m && sc < 0) sc = b0 + __ffs(m) - 1;
+      }
+      return sc >= 0 ? f * RN + sc : RN * RN;
+    };
+    int32_t rpair = RN && has ? ring_pair() : 0;
+    uint32_t rrun = 0;
+
     // histogram windows: row-lane q counts values base+q and base+16+q
     uint32_t hc0 = 0, hc1 = 0, hb0 = 0, hb1 = 0;
     int32_t base_c = max(0, cut - 16), base_b = max(0, bnodes - 16);
     auto observe = [&](bool on) {
       if (!on) return;
+      if (FULL) rrun += 1;
       sum_cut += cut;
       sum_bnodes += bnodes;
       sum_invb += invb;
@@ -973,6 +996,14 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x112, 0xF, 0xF, true);
       dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x114, 0xF, 0xF, true);
       const int dnp = (int)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x154, 0xF, 0xF, false);  // row_newbcast:4
+      if (FULL && RN && accepted && p.ring_node[v]) {  // only a ring node's flip moves the pair
+        const int32_t np2 = ring_pair();
+        if (np2 != rpair) {
+          if (q == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
+          rrun = 0;
+          rpair = np2;
+        }
+      }
       STAMP(9);  // commit
       if (accepted) {
         n_acc += 1;
@@ -1001,6 +1032,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (hc1) atomicAdd(p.hist_cut + base_c + ROW + q, (unsigned long long)hc1);
       if (hb0) atomicAdd(p.hist_b + base_b + q, (unsigned long long)hb0);
       if (hb1) atomicAdd(p.hist_b + base_b + ROW + q, (unsigned long long)hb1);
+      if (FULL && RN && q == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
       for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
@@ -1078,7 +1110,8 @@ bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop) {
 }
 
 void* fw_grid16_fn(const FwRunParams& p) {
-  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr;
+  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
+                    p.ring_n > 0;
   return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
 }
 

@@ -87,6 +87,14 @@ struct FwRunParams {
   int32_t accept;
   const uint8_t* flags;
   int32_t* bcnt;
+  // district-shape observable (fw_chains_enable_ring; ring_n == 0: off): ring edge r joins
+  // ring_u[r] and ring_w[r]; ring_node[x] = 1 iff x is an endpoint of a ring edge; yields
+  // counted per pair of first two cut ring edges, index i*ring_n + j (ring_n^2: < 2 cut)
+  int32_t ring_n;
+  const int32_t* ring_u;
+  const int32_t* ring_w;
+  const uint8_t* ring_node;
+  unsigned long long* hist_ring;  // [ring_n^2 + 1]
 };
 
 // fw_chains_read_map: finalise maps of a chain range (see include/flipwalk.h)
@@ -132,6 +140,7 @@ int fw_launch_bcnt_init(const FwRunParams& p, void* stream);
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);
+int fw_run_gsum_words(int G);
 // fw_grid16.hip
 bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop);
 void* fw_grid16_fn(const FwRunParams& p);

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         uint32_t w = 0, cd = 0;
         if (x < n) C.template weight_now<MODE>(x, w, cd);
         const uint32_t gsum_t = wave_sum(w);
-        if (lane == 0) C.gsum[t] = gsum_t;
+        if (lane == 0) C.gsum[gsum_slot<PER>(t)] = gsum_t;
         cut2 += cd;
         bn += cd > 0;
         np += w;
@@ -117,11 +117,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     lds_order();
     double invb = p.g.invb[bnodes];  // 1/|B| from the graph's table (|B| > 0 for k >= 2)
 
+    // district-shape observable: the pair of the first two cut ring edges (ring order),
+    // counted per yield in runs (a pair changes only when an accepted flip moves a ring
+    // node), flushed to the ring histogram when it changes and at the end of the launch
+    const int RN = p.ring_n;
+    auto ring_pair = [&]() -> int32_t {  // wave-uniform; labels must be clean (no search marks)
+      int f = -1, sc = -1;
+      for (int b0 = 0; b0 < RN && sc < 0; b0 += WAVE) {
+        const int r = b0 + lane;
+        const int ri = r < RN ? r : 0;
+        uint64_t m = ballot(r < RN && C.L(p.ring_u[ri]) != C.L(p.ring_w[ri]));
+        if (m && f < 0) {
+          f = b0 + __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+        }
+        if (m) sc = b0 + __ffsll((unsigned long long)m) - 1;
+      }
+      return sc >= 0 ? f * RN + sc : RN * RN;
+    };
+    int32_t rpair = RN ? ring_pair() : 0;
+    uint32_t rrun = 0;
+
     // histogram windows: lane i counts value base+i
     uint32_t hc = 0, hb = 0;
     int32_t base_c = max(0, cut - 32), base_b = max(0, bnodes - 32);
     auto observe = [&]() {
       n_yield += 1;
+      rrun += 1;
       sum_cut += cut;
       sum_bnodes += bnodes;
       sum_invb += invb;
@@ -281,7 +303,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (p.sched) sched_row(n_acc);
         n_adeg += (uint32_t)dv;
         if (lane == 0) PK<LB>::axor(C.lab, v, a ^ d);
-        if (mine && h.x >= 0 && wn != wo) lds_add(C.gsum + (h.x >> 6), wn - wo);
+        if (mine && h.x >= 0 && wn != wo) lds_add(C.gsum + gsum_slot<PER>(h.x >> 6), wn - wo);
         lds_order();
         npairs += (int32_t)wave_sum(mine ? wn - wo : 0u);
         cut += dcut;
@@ -294,6 +316,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           if (lane == (int)a) bcnt -= 1;
           if (lane == (int)d) bcnt += 1;
         }
+        if (RN && p.ring_node[v]) {  // only a flip of a ring node can change the pair
+          const int32_t np2 = ring_pair();
+          if (np2 != rpair) {
+            if (lane == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
+            rrun = 0;
+            rpair = np2;
+          }
+        }
       }
       observe();
     }
@@ -301,6 +331,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // ---- write back
     if (hc) atomicAdd(p.hist_cut + base_c + lane, (unsigned long long)hc);
     if (hb) atomicAdd(p.hist_b + base_b + lane, (unsigned long long)hb);
+    if (RN && lane == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
     {
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(C.lab);
@@ -448,12 +479,26 @@ __global__ void fw_map_read_kernel(FwMapRead m) {
   }
 }
 
+}  // namespace
+
+// group sums per lane of the one-chain-per-wave kernel (pick_per) and the LDS words its
+// padded level-1 layout (gsum_slot) takes for G groups
+int fw_run_per(int G) { return G <= 64 * 2 ? 2 : G <= 64 * 4 ? 4 : G <= 64 * 8 ? 8 : 16; }
+int fw_run_gsum_words(int G) {
+  const int per = fw_run_per(G);
+  return G <= 0 ? 0 : ((G - 1) / per) * (per + 1) + (G - 1) % per + 1;
+}
+
+namespace {
+
 template <int LB, bool GRID, int MODE, bool E16, int WPE = 4>
 void* pick_per(int G) {
-  if (G <= 64 * 2) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE>);
-  if (G <= 64 * 4) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE>);
-  if (G <= 64 * 8) return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE>);
-  return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE>);
+  switch (fw_run_per(G)) {
+    case 2: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE>);
+    case 4: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE>);
+    case 8: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE>);
+    default: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE>);
+  }
 }
 
 // grids: implicit neighbours; general graphs: the padded 16-wide table when it exists

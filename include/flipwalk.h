@@ -86,6 +86,23 @@ extern "C" {
 #define FW_READ_HIST_CUT 2 /* uint64 [n_edges+1]  yields with |cut edges| = i */
 #define FW_READ_HIST_B 3   /* uint64 [n+1]        yields with |B| = i         */
 #define FW_READ_POPS 4     /* int64  [n_chains][k] district populations       */
+#define FW_READ_HIST_RING 5 /* uint64 [n_ring*n_ring+1] yields per ring pair (below) */
+#define FW_READ_RING_PAIR 6 /* int32  [n_chains][2] current ring pair (i, j), -1 = none */
+
+/* ---- district-shape observable (fw_chains_enable_ring) ----------------------
+ * boundary_slope (grid_chain_sec11.py:55-78; Frankenstein_chain.py:57-80) collects the
+ * cut edges that lie on the outer ring of the grid (both endpoints in its first/last row
+ * or column, plus the four corner diagonals of the sec11 graph); the driver (:371-394)
+ * takes the first two, temp[0] and temp[1], and records the slope of the line through
+ * their midpoints and the angle they subtend at the grid centre, once per yield.  The
+ * kernels keep, per yield, the pair (i, j), i < j, of the first two CUT ring edges in the
+ * caller's ring order and count yields per pair: FW_READ_HIST_RING index i*n_ring + j,
+ * index n_ring*n_ring for yields with fewer than two cut ring edges (the reference would
+ * raise IndexError there).  The host turns pairs into slopes and angles with the
+ * reference's own float formula.  With exactly two cut ring edges (a two-district plan
+ * whose boundary crosses the ring twice) the result does not depend on the order;
+ * with more, the reference picks by CPython set-iteration order, which depends on the
+ * interpreter's tuple hash, and the build picks the first two in ring order.            */
 
 /* ---- spatial observables (fw_chains_enable_maps / fw_chains_read_map) ------
  * The reference driver's per-edge and per-node maps, updated once per yield
@@ -131,8 +148,8 @@ typedef struct fw_chains fw_chains;
 /* Thread-local description of the last error on this thread. */
 const char* fw_last_error(void);
 
-/* Library/ABI version, e.g. 0x000300 for 0.3.0 (0.2: spatial maps; 0.3: bound
- * schedules). */
+/* Library/ABI version, e.g. 0x000400 for 0.4.0 (0.2: spatial maps; 0.3: bound
+ * schedules; 0.4: ring observable, checkpoint/resume). */
 int32_t fw_version(void);
 
 /* Number of visible HIP devices (0 when none; never fails). */
@@ -190,6 +207,17 @@ int fw_chains_run_traced(fw_chains* c, int64_t steps, int32_t max_retries, int32
 /* Copy a state array back to the host (see FW_READ_*). */
 int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes);
 
+/* Overwrite a state array from the host: the inverse of fw_chains_read, for exact
+ * checkpoint / resume (the chain states plus the Philox attempt counter in
+ * the stats record are a complete checkpoint of the counter-based RNG).  what is
+ * FW_READ_LABELS (every plan is validated like an initial state, FW_ESTATE otherwise, and
+ * the district populations are recomputed from it), FW_READ_STATS (counters, sums and
+ * the attempt counter; the stuck flag included), FW_READ_HIST_CUT, FW_READ_HIST_B or
+ * FW_READ_HIST_RING.  A chain resumed from {labels, stats} continues exactly as the
+ * uninterrupted chain (same proposals, same Metropolis draws).  The spatial maps and the
+ * FW_ACCEPT_BOUNDARY counts are not part of a checkpoint. */
+int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t bytes);
+
 /* Zero the per-chain sums and the yield histograms (not the chain states). */
 int fw_chains_reset_observables(fw_chains* c);
 
@@ -213,6 +241,12 @@ int fw_chains_set_schedule(fw_chains* c, const double* rows, int32_t n_rows, int
  * (e.g. {-1, 1} for the reference's k=2 plans); NULL means 0..k-1.  Costs
  * 8*n_edges + 16*n bytes of HBM per chain.  Yields per chain must stay below 2^32. */
 int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values);
+
+/* Turn on the district-shape observable for every chain: ring edge r joins nodes
+ * ring_u[r] and ring_w[r] (an edge of the graph; 2 <= n_ring <= 1024), in the order that
+ * picks "the first two".  Zeroes the ring histogram; may be called between runs. */
+int fw_chains_enable_ring(fw_chains* c, const int32_t* ring_u, const int32_t* ring_w,
+                          int32_t n_ring);
 
 /* Read a map (FW_MAP_*) of chains [chain0, chain0 + n_chains) as int64
  * [n_chains][len], or with FW_MAP_SUM its sum over those chains [len]; len is

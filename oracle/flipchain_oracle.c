@@ -111,6 +111,7 @@ typedef struct {
   uint64_t* hist_cut; /* may be NULL */
   uint64_t* hist_b;   /* may be NULL */
   struct orc_maps* maps; /* may be NULL */
+  const struct orc_ring* ring; /* may be NULL */
   int32_t accept_rule;   /* FW_ACCEPT_* */
   const double* sched;   /* fw_chains_set_schedule rows [sched_rows][2*maxdeg+1] or NULL */
   int32_t sched_rows;
@@ -138,6 +139,17 @@ typedef struct orc_maps {
   int32_t cur_f;             /* creating flip of the current state, -1: none (initial) */
   int32_t pad;
 } orc_maps;
+
+/* The district-shape observable of boundary_slope (grid_chain_sec11.py:55-78) and the
+ * driver's slope/angle block (:371-394): once per yield, the pair (i, j), i < j, of the
+ * first two cut ring edges in ring order, counted in hist[i*n_ring + j] (hist[n_ring^2]:
+ * fewer than two).  Ring edge r joins u[r] and w[r].  A literal per-yield scan. */
+typedef struct orc_ring {
+  const int32_t* u;
+  const int32_t* w;
+  int32_t n_ring, pad;
+  uint64_t* hist; /* [n_ring*n_ring + 1] */
+} orc_ring;
 
 static inline int64_t popof(const graph_t* g, int32_t v) { return g->pop ? g->pop[v] : 1; }
 
@@ -479,8 +491,22 @@ static void maps_yield(chain_t* c) {
   }
 }
 
+static void ring_yield(chain_t* c) {
+  const orc_ring* R = c->ring;
+  int32_t first = -1, second = -1;
+  for (int32_t r = 0; r < R->n_ring && second < 0; ++r)
+    if (c->lab[R->u[r]] != c->lab[R->w[r]]) {
+      if (first < 0)
+        first = r;
+      else
+        second = r;
+    }
+  R->hist[second >= 0 ? (int64_t)first * R->n_ring + second : (int64_t)R->n_ring * R->n_ring]++;
+}
+
 static void yield_obs(chain_t* c) {
   if (c->maps) maps_yield(c);
+  if (c->ring) ring_yield(c);
   c->st.yields++;
   c->st.sum_cut += c->st.cut;
   c->st.sum_bnodes += c->st.bnodes;
@@ -577,7 +603,8 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
                      fw_chain_stats* stats, int64_t steps, int32_t max_retries,
                      uint64_t* hist_cut, uint64_t* hist_b, int32_t* trace, int64_t* pops_out,
                      orc_maps* maps, int32_t accept_rule, const uint8_t* flags,
-                     const double* sched, int32_t sched_rows, int64_t sched_t0) {
+                     const double* sched, int32_t sched_rows, int64_t sched_t0,
+                     const orc_ring* ring) {
   chain_t c;
   if (setup(&c, rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr)) {
     teardown(&c);
@@ -590,6 +617,7 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
   c.hist_cut = hist_cut;
   c.hist_b = hist_b;
   c.maps = maps;
+  c.ring = ring;
   c.accept_rule = accept_rule;
   c.flags = flags;
   c.sched = sched_rows > 0 ? sched : NULL;
@@ -662,7 +690,7 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
                   uint64_t* hist_b, int32_t* trace, int64_t* pops_out) {
   return orc_run_chain_ex(rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr, seed,
                           chain_id, labels, stats, steps, max_retries, hist_cut, hist_b, trace,
-                          pops_out, NULL, FW_ACCEPT_CUT, NULL, NULL, 0, 0);
+                          pops_out, NULL, FW_ACCEPT_CUT, NULL, NULL, 0, 0, NULL);
 }
 
 /* Per-flip evaluation on one state (the fw_eval_flips contract). */

@@ -66,7 +66,7 @@ def lib():
         ]
         L.orc_run_chain.restype = ctypes.c_int
         L.orc_run_chain_ex.argtypes = L.orc_run_chain.argtypes + [
-            _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int64]
+            _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int64, _P]
         L.orc_run_chain_ex.restype = ctypes.c_int
         L.orc_eval_flips.argtypes = [
             _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
@@ -130,16 +130,34 @@ class Maps:
         return ps
 
 
+class _OrcRing(ctypes.Structure):
+    _fields_ = [("u", _P), ("w", _P), ("n_ring", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("hist", _P)]
+
+
+class Ring:
+    """The district-shape observable (boundary_slope, grid_chain_sec11.py:55-78 and the
+    driver's :371-394): yields per pair of first two cut ring edges, ring order."""
+
+    def __init__(self, ring_u, ring_w):
+        self.u = np.ascontiguousarray(ring_u, np.int32)
+        self.w = np.ascontiguousarray(ring_w, np.int32)
+        n = len(self.u)
+        self.hist = np.zeros(n * n + 1, np.uint64)
+        self._s = _OrcRing(_ptr(self.u), _ptr(self.w), n, 0, _ptr(self.hist))
+
+
 def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps,
               max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False,
-              maps=None, accept_rule=0, flags=None, schedule=None):
+              maps=None, accept_rule=0, flags=None, schedule=None, ring=None):
     """Run one chain on the CPU oracle.  ``graph`` needs rowptr/col/pop/n/grid_w.
 
     Returns (labels, stats, pops, trace-or-None); ``labels`` is a new int16 array.
     ``maps`` (an oracle ``Maps``) accumulates the per-yield spatial observables;
     ``accept_rule`` is FW_ACCEPT_* (0 cut_accept, 1 the |B'|/|B| rule, 2 uniform_accept
     with boundary_condition over the uint8 ``flags``).  ``schedule`` = (rows, t0): the
-    step-dependent bounds of fw_chains_set_schedule.
+    step-dependent bounds of fw_chains_set_schedule; ``ring`` (an oracle ``Ring``)
+    accumulates the district-shape observable.
     """
     srows, st0 = (None, 0) if schedule is None else schedule
     if srows is not None:
@@ -156,6 +174,7 @@ def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps
         int(steps), int(max_retries), _ptr(hist_cut), _ptr(hist_b), _ptr(tr), _ptr(pops),
         None if maps is None else ctypes.byref(maps._s), int(accept_rule), _ptr(fl),
         _ptr(srows), 0 if srows is None else int(srows.shape[0]), int(st0),
+        None if ring is None else ctypes.byref(ring._s),
     )
     if rc != 0:
         raise MemoryError("oracle allocation failed")

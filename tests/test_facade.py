@@ -135,10 +135,10 @@ def test_reference_driver_loop_matches_gpu_maps(gpu_lib):
             i, j = idx[a], idx[b]
             cut_times[eid[(min(i, j), max(i, j))]] += 1
         temp = p["slope"]
-        if len(temp) >= 2:
-            s_, a_ = gc.slope_and_angle(temp)
-            slopes.append(s_)
-            angles.append(a_)
+        assert len(temp) == 2
+        s_, a_ = gc.slope_and_angle(temp)
+        slopes.append(s_)
+        angles.append(float(a_))
         if p.flips is not None:
             f = idx[list(p.flips.keys())[0]]
             part_sum[f] -= p.assignment[g.nodes[f]] * (t - last_flipped[f])
@@ -149,6 +149,20 @@ def test_reference_driver_loop_matches_gpu_maps(gpu_lib):
     never = last_flipped == 0
     part_sum[never] = t * np.array([final.assignment[g.nodes[x]] for x in np.flatnonzero(never)])
     res = mk().run_batched(1, chain_id0=0, maps=True)
+    # A15 on the GPU: the chain's ring-pair histogram, turned into (slope, angle) with the
+    # reference's expressions, is the multiset the literal loop recorded (every state here
+    # crosses the ring exactly twice, so the pick of "the first two" is order-free)
+    from flipcomplexityempirical_amd import shape
+    ru, rw = shape.ring_edges(g, shape.sec11_on_ring(39))
+    ch = mk()._make(1, 0)
+    ch.enable_ring(ru, rw)
+    ch.run(1199)
+    s_g, a_g, c_g, short = shape.shape_samples(ch.hist_ring(), g, ru, rw)
+    ch.close()
+    assert short == 0 and c_g.sum() == t
+    got = sorted(zip(np.repeat(s_g, c_g).tolist(), np.repeat(a_g, c_g).tolist()))
+    want = sorted(zip(slopes, angles))
+    assert len(got) == len(want) and all(x == y for x, y in zip(got, want))
     assert np.array_equal(res.maps["cut_times"][0], cut_times)
     assert np.array_equal(res.maps["num_flips"][0], num_flips)
     assert np.array_equal(res.maps["last_flipped"][0], last_flipped)

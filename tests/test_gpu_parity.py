@@ -383,3 +383,40 @@ def test_long_run_split_into_launches(gpu_lib, name, path, monkeypatch):
     monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
     case = {c.name: c for c in CASES}[name]
     _run_vs_oracle(case, 11, [1000, 333])
+
+
+@pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
+                                       ("sec11_a2_k2", "auto"), ("tract_k4", "auto")])
+def test_checkpoint_resume_bit_exact(gpu_lib, name, path, monkeypatch, tmp_path):
+    """SURVEY.md §5 checkpoint / resume: plans + stats (with the Philox attempt counter) +
+    histograms saved to an .npz (no pickle) after 300 steps and loaded into a NEW handle;
+    400 more steps there equal 400 more steps of the uninterrupted handle, bit for bit."""
+    from flipcomplexityempirical_amd import shape
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    g = case.graph
+    dg = DeviceGraph(g)
+    ch = Chains(dg, 12, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                base=case.base, seed=71, chain_id0=9)
+    ring = name.startswith("sec11")
+    if ring:
+        ch.enable_ring(*shape.ring_edges(g, shape.sec11_on_ring(39)))
+    ch.run(300)
+    path_ck = str(tmp_path / "ck.npz")
+    ch.save_checkpoint(path_ck)
+    ch.run(400)
+    ch2 = Chains.from_checkpoint(dg, path_ck, case.k, proposal=case.mode, pop_bounds=case.bounds)
+    ch2.run(400)
+    assert np.array_equal(ch.labels(), ch2.labels())
+    assert ch.stats().tobytes() == ch2.stats().tobytes()
+    assert np.array_equal(ch.pops(), ch2.pops())
+    assert np.array_equal(ch.hist_cut(), ch2.hist_cut())
+    assert np.array_equal(ch.hist_b(), ch2.hist_b())
+    if ring:
+        assert np.array_equal(ch.hist_ring(), ch2.hist_ring())
+    # the resumed run is also the oracle's uninterrupted 700-step run
+    _, ost = oracle_chains(case, 71, range(9, 21), [700])[:2]
+    assert_stats_equal(ch2.stats(), ost)
