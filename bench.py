@@ -176,6 +176,12 @@ def main():
                     help="strong: --chains (default: the configuration's) in total, sharded; "
                          "weak: --chains per GPU")
     ap.add_argument("--chains", type=int, default=None)
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="run only rank R's shard of an N-GPU job, standalone on this GPU (one "
+                         "line per shard; the N-GPU job's rate is total steps / max shard time: "
+                         "scripts/shards.sh)")
+    ap.add_argument("--ladder", default="interleaved", choices=["interleaved", "contiguous"],
+                    help="C5: base groups spread over the shards (default) or adjacent (round 1)")
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--base", type=float, default=None)
@@ -197,6 +203,11 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    shard_rank, shard_world = rank, world
+    if args.shard:
+        if world > 1:
+            raise SystemExit("--shard emulates one rank of a job: run it as a single process")
+        shard_rank, shard_world = (int(x) for x in args.shard.split("/"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = 0 if args.same_device else local_rank
     import torch
@@ -210,16 +221,17 @@ def main():
     from flipcomplexityempirical_amd.distributed import merge_histograms, shard_range
 
     w = workload(args.config, args.grid, args.k)
+    w.interleave = args.ladder == "interleaved"
     g, init, k = w.graph, w.init, w.k
     proposal = args.proposal or w.proposal
     percent = args.percent if args.percent is not None else w.percent
     if args.scaling == "strong":
         total = args.chains or w.chains
-        lo, hi = shard_range(total, world, rank)
+        lo, hi = shard_range(total, shard_world, shard_rank)
     else:
         per = args.chains or w.chains
-        total = per * world
-        lo, hi = rank * per, (rank + 1) * per
+        total = per * shard_world
+        lo, hi = shard_rank * per, (shard_rank + 1) * per
     chains = hi - lo
     if args.base is not None:
         base, base_desc = args.base, f"base {args.base:.9g}"
@@ -289,7 +301,10 @@ def main():
                      "rocprof_kernel_ms": (tj.get("kernel_trace") or {}).get("avg_ms")}
 
     if rank == 0:
-        if dist is None:
+        if args.shard:
+            par = (f"shard {shard_rank} of {shard_world} (global chain ids [{lo}, {hi})) run "
+                   f"standalone on 1 GPU: one rank of the {shard_world}-GPU job")
+        elif dist is None:
             par = "1 GPU"
         elif args.same_device:
             par = (f"REHEARSAL: {world} ranks on ONE device (same device, {args.backend} "
@@ -318,6 +333,8 @@ def main():
                             f"contiguity",
                 "chains_total": total,
                 "chains_per_gpu": chains,
+                "shard": args.shard,
+                "ladder": args.ladder if w.base is None else None,
                 "spatial_maps": bool(args.maps),
                 "flip_steps_per_chain_per_step": args.inner,
                 "parallelism": par,
@@ -343,7 +360,7 @@ def main():
             "mean_bnodes": float(st1_arr["bnodes"].mean()),
             "hist_yields": int(hist_cut.sum()),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.shard and not args.no_cpu_baseline:
             b0 = float(np.ravel(base)[0])
             out["cpu_baseline"] = cpu_baseline(args.config, w.desc, percent, b0, args.seed,
                                                seconds=args.cpu_seconds)

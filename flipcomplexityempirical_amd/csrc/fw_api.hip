@@ -187,17 +187,25 @@ int pick_lb(int k, int maxdeg) {
   return 0;
 }
 
-// LB-bit little-endian fields: node x in bits [x*LB, x*LB + LB) of the byte stream.
+// LB-bit little-endian fields: node x in bits [x*LB, x*LB + LB) of the byte stream (a
+// 3-bit field may straddle two bytes; the label region is padded past its last field).
 void pack_labels(const int16_t* lab, int n, int lb, uint8_t* out, int bytes) {
   std::memset(out, 0, (size_t)bytes);
-  const int per = 8 / lb;
-  for (int x = 0; x < n; ++x)
-    out[x / per] |= (uint8_t)((lab[x] & ((1 << lb) - 1)) << ((x % per) * lb));
+  for (int x = 0; x < n; ++x) {
+    const int64_t bit = (int64_t)x * lb;
+    const uint32_t v = (uint32_t)(lab[x] & ((1 << lb) - 1)) << (bit & 7);
+    out[bit >> 3] |= (uint8_t)v;
+    if ((bit & 7) + lb > 8) out[(bit >> 3) + 1] |= (uint8_t)(v >> 8);
+  }
 }
 
 void unpack_labels(const uint8_t* in, int n, int lb, int16_t* lab) {
-  const int per = 8 / lb;
-  for (int x = 0; x < n; ++x) lab[x] = (in[x / per] >> ((x % per) * lb)) & ((1 << lb) - 1);
+  for (int x = 0; x < n; ++x) {
+    const int64_t bit = (int64_t)x * lb;
+    uint32_t v = in[bit >> 3];
+    if ((bit & 7) + lb > 8) v |= (uint32_t)in[(bit >> 3) + 1] << 8;
+    lab[x] = (int16_t)((v >> (bit & 7)) & ((1u << lb) - 1));
+  }
 }
 
 // MarkovChain's initial-state validity: every district non-empty, connected and
@@ -468,7 +476,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   for (int x = 0; x < n; ++x) total_pop += g->popof(x);
   const bool use16 = fw_grid16_candidate(g->gw, D, G, k, total_pop) && g->gm24 != 0 &&
                      !(no16 && no16[0] == '1');
-  const int lb = use16 ? (k <= 4 ? 2 : 4) : pick_lb(k, g->maxdeg);
+  const int lb = use16 ? fw_grid16_lb(G, k) : pick_lb(k, g->maxdeg);
   if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 
   auto c = new fw_chains();
@@ -491,6 +499,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   {  // FLIPWALK_NO_BITBOARD=1: the grid kernel runs every exact search as the list search
     const char* e = getenv("FLIPWALK_NO_BITBOARD");
     p.no_bb = e && e[0] == '1' ? 1 : 0;
+    const char* e2 = getenv("FLIPWALK_NO_ROWBB");
+    p.no_rowbb = e2 && e2[0] == '1' ? 1 : 0;
   }
   // +8: the grid kernels read label dwords one past the last node
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
@@ -629,8 +639,8 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
     const int64_t s = left < cap ? left : cap;
     c->p.steps = s;
     HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
-    if (fw_launch_run(c->p, c->lb, c->grid, c->stream) != 0)
-      return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    const int le = fw_launch_run(c->p, c->lb, c->grid, c->stream);
+    if (le != 0) return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString((hipError_t)le));
     left -= s;
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -820,7 +830,8 @@ int fw_chains_reset_observables(fw_chains* c) {
     HIPCHK(hipMemset(c->d_acc, 0, sizeof(int64_t) * std::max<size_t>(C * E, 1)));
     HIPCHK(hipMemset(c->d_nf, 0, sizeof(uint32_t) * C * n));
     HIPCHK(hipMemset(c->d_lf, 0, sizeof(uint32_t) * C * n));
-    if (fw_launch_map_init(c->p, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess)
+    if (fw_launch_map_init(c->p, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
       return fail(FW_EHIP, "map re-init failed");
     c->max_yields = 0;
   }
@@ -849,7 +860,8 @@ int fw_chains_set_accept(fw_chains* c, int32_t rule, const uint8_t* node_flags) 
     HIPCHK(hipMemset(c->d_bcnt, 0, nb));
     c->p.flags = c->d_flags;
     c->p.bcnt = c->d_bcnt;
-    if (fw_launch_bcnt_init(c->p, c->stream) != 0 || hipStreamSynchronize(c->stream) != hipSuccess)
+    if (fw_launch_bcnt_init(c->p, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
       return fail(FW_EHIP, "flag count init failed");
   }
   c->p.accept = rule;
@@ -922,8 +934,8 @@ int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values) {
   p.m_ps = c->d_ps;
   p.m_pend = c->d_pend;
   p.m_labval = c->d_labval;
-  if (fw_launch_map_init(p, c->stream) != 0)
-    return fail(FW_EHIP, "map init launch failed: %s", hipGetErrorString(hipGetLastError()));
+  const int le = fw_launch_map_init(p, c->stream);
+  if (le != 0) return fail(FW_EHIP, "map init launch failed: %s", hipGetErrorString((hipError_t)le));
   HIPCHK(hipStreamSynchronize(c->stream));
   return FW_OK;
 }
@@ -1007,8 +1019,9 @@ int fw_chains_read_map(fw_chains* c, int32_t what, int32_t chain0, int32_t n_cha
   m.n_chains = n_chains;
   m.out = d_out;
   int rc = FW_OK;
-  if (fw_launch_map_read(m, c->stream) != 0)
-    rc = fail(FW_EHIP, "map read launch failed: %s", hipGetErrorString(hipGetLastError()));
+  const int le = fw_launch_map_read(m, c->stream);
+  if (le != 0)
+    rc = fail(FW_EHIP, "map read launch failed: %s", hipGetErrorString((hipError_t)le));
   else if (hipMemcpyAsync(dst, d_out, need, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
            hipStreamSynchronize(c->stream) != hipSuccess)
     rc = fail(FW_EHIP, "map download failed");
@@ -1085,8 +1098,8 @@ int fw_eval_flips(fw_graph* g, const int16_t* labels, int32_t k, const int32_t* 
     p.spill = d_spill;
     if (!ok) {
       rc = fail(FW_EHIP, "upload failed in fw_eval_flips");
-    } else if (fw_launch_eval(p, lb, grid, nullptr) != 0) {
-      rc = fail(FW_EHIP, "eval launch failed: %s", hipGetErrorString(hipGetLastError()));
+    } else if (const int le = fw_launch_eval(p, lb, grid, nullptr)) {
+      rc = fail(FW_EHIP, "eval launch failed: %s", hipGetErrorString((hipError_t)le));
     } else if (hipDeviceSynchronize() != hipSuccess) {
       rc = fail(FW_EHIP, "eval kernel failed: %s", hipGetErrorString(hipGetLastError()));
     } else {

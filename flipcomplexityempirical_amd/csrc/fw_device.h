@@ -159,6 +159,27 @@ struct PK {
   }
 };
 
+// 3-bit labels (k <= 8 on the grid kernel's large-grid plan): node x in bits [3x, 3x+3) of
+// a little-endian dword stream, so a field may straddle two dwords.  Reads take the dword
+// pair (one ds_read2_b32; the label region is padded past its last field); an update xors
+// each dword the field touches (two atomics for a straddling field).
+template <>
+struct PK<3> {
+  static constexpr uint32_t MASK = 7u;
+  __device__ static __forceinline__ uint32_t get(const LDS uint8_t* b, int x) {
+    const LDS uint32_t* w = reinterpret_cast<const LDS uint32_t*>(b);
+    const int bit = 3 * x, wi = bit >> 5;
+    const uint64_t both = ((uint64_t)w[wi + 1] << 32) | w[wi];
+    return (uint32_t)(both >> (bit & 31)) & 7u;
+  }
+  __device__ static __forceinline__ void axor(LDS uint8_t* b, int x, uint32_t d) {
+    LDS uint32_t* w = reinterpret_cast<LDS uint32_t*>(b);
+    const int bit = 3 * x, wi = bit >> 5, sh = bit & 31;
+    __atomic_fetch_xor(w + wi, d << sh, __ATOMIC_RELAXED);
+    if (sh > 29) __atomic_fetch_xor(w + wi + 1, d >> (32 - sh), __ATOMIC_RELAXED);
+  }
+};
+
 __device__ __forceinline__ void lds_add(LDS uint32_t* p, uint32_t v) {
   __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
@@ -300,9 +321,33 @@ __device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int
   uint32_t wd[LB + 1];
 #pragma unroll
   for (int j = 0; j <= LB; ++j) wd[j] = w[min(max(wi + j, 0), wlast)];
+  if constexpr (LB == 3) {
+    // realign the 96 bits of the 32 fields to bit 0, then one field per bit-field extract
+    const uint32_t r0 = __builtin_amdgcn_alignbit(wd[1], wd[0], sh);
+    const uint32_t r1 = __builtin_amdgcn_alignbit(wd[2], wd[1], sh);
+    const uint32_t r2 = __builtin_amdgcn_alignbit(wd[3], wd[2], sh);
+    uint32_t out3 = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int pos = 3 * j;
+      uint32_t f;
+      if (pos + 3 <= 32)
+        f = (r0 >> pos) & 7u;
+      else if (pos < 32)
+        f = ((r0 >> pos) | (r1 << (32 - pos))) & 7u;
+      else if (pos + 3 <= 64)
+        f = (r1 >> (pos - 32)) & 7u;
+      else if (pos < 64)
+        f = ((r1 >> (pos - 32)) | (r2 << (64 - pos))) & 7u;
+      else
+        f = (r2 >> (pos - 64)) & 7u;
+      out3 |= (f == a ? 1u : 0u) << j;
+    }
+    return out3;
+  }
   uint32_t out = 0;
 #pragma unroll
-  for (int j = 0; j < LB; ++j) {  // 32 / LB labels per aligned dword
+  for (int j = 0; j < (LB == 3 ? 0 : LB); ++j) {  // 32 / LB labels per aligned dword
     const uint32_t x = __builtin_amdgcn_alignbit(wd[j + 1], wd[j], sh);
     uint32_t e;
     if constexpr (LB == 2) {
@@ -319,7 +364,7 @@ __device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int
       e = (e | (e >> 6)) & 0x000F000Fu;
       e = (e | (e >> 12)) & 0x000000FFu;
     } else {
-      static_assert(LB == 8, "labels are 2, 4 or 8 bits");
+      static_assert(LB == 8 || LB == 3, "labels are 2, 3, 4 or 8 bits");
       const uint32_t y = x ^ (a * 0x01010101u);
       e = (~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u) >> 7;
       e = (e | (e >> 7)) & 0x00030003u;

@@ -21,6 +21,9 @@
 // observables), reference grid_chain_sec11.py:117-179,340-402.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "fw_device.h"
 
 #ifdef FW_STAMPS
@@ -282,6 +285,129 @@ __device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bo
   return full ? 1 : (closed ? 0 : -1);
 }
 
+// grid_race_bb (fw_device.h) run by every row at once on its own chain, in a 16-row x
+// 32-column window: row-lane q holds grid row vr - 8 + q, bit b column vc - 16 + b.  The
+// same level-synchronous race on bitboards, with row-level DPP shifts and row ballots, so
+// the four chains of a wave search side by side instead of one after another (C5's
+// fractal low-base chains need an exact search on a quarter of their steps).  Rows with
+// need == false return -1 untouched; a row returns 1 / 0 (connected / disconnected, with
+// its dequeued cells and their degrees in nodes / degs, row-uniform) or -1 when a
+// frontier about to be processed reaches a window-edge cell with an on-grid neighbour
+// outside (nothing counted: the caller continues with the 64x32 wave form).  Whatever the
+// window, the processed levels are the list search's, so the verdicts and counters are
+// bit-identical to the oracle's.
+__device__ __forceinline__ uint32_t from_prev_row_lane(uint32_t x) {  // row_shr:1, 0 at lane 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t from_next_row_lane(uint32_t x) {  // row_shl:1, 0 at lane 15
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dilate_row(uint32_t x) {
+  return x | (x << 1) | (x >> 1) | from_prev_row_lane(x) | from_next_row_lane(x);
+}
+
+template <int LB>
+__device__ int grid_race_bb_row(const LDS uint8_t* lab, int n, int W, int H, int q, int row,
+                                bool need, int vr, int vc, uint32_t a, uint32_t am4, uint32_t lk,
+                                uint32_t& nodes, uint32_t& degs) {
+  const int r = vr - 8 + q, c0 = vc - 16;
+  const bool rin = (r >= 0) & (r < H);
+  uint32_t A = eq_bits32<LB>(lab, n, (rin ? r : vr) * W + c0, a);
+  const int lo_cut = c0 < 0 ? -c0 : 0;  // bits of columns < 0
+  const int hi_n = W - c0;              // bits >= hi_n: columns >= W (hi_n >= 17)
+  uint32_t cm = ~0u << lo_cut;
+  if (hi_n < 32) cm &= (1u << hi_n) - 1u;
+  A &= rin ? cm : 0u;
+  if (q == 8) A &= ~(1u << 16);  // v
+  uint32_t E = ((q == 0) & (r > 0)) | ((q == 15) & (r < H - 1)) ? ~0u : 0u;
+  if (c0 > 0) E |= 1u;
+  if (c0 + 31 < W - 1) E |= 1u << 31;
+  E &= A;
+  uint32_t F[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {  // sources up (7, 16), left (8, 15), right (8, 17), down (9, 16)
+    const int sl = d == 0 ? 7 : (d == 3 ? 9 : 8), sb = d == 1 ? 15 : (d == 2 ? 17 : 16);
+    F[d] = (q == sl && ((am4 >> d) & 1u)) ? (1u << sb) : 0u;
+  }
+  uint32_t M = 0x8421u;  // class of direction d: 4-bit member mask at bits 4d (row-uniform)
+  auto unite = [&](int i, int j) {
+    const uint32_t m = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      M = ((m >> d) & 1u) ? (M & ~(15u << (4 * d))) | (m << (4 * d)) : M;
+  };
+  if (lk & 1u) unite(0, 2);  // N-E
+  if (lk & 2u) unite(2, 3);  // E-S
+  if (lk & 4u) unite(3, 1);  // S-W
+  if (lk & 8u) unite(1, 0);  // W-N
+  auto n_classes = [&]() {
+    int nc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      nc += (int)(((am4 >> d) & 1u) && (__ffs((M >> (4 * d)) & 15u) - 1) == d);
+    return nc;
+  };
+  uint32_t V = F[0] | F[1] | F[2] | F[3];
+  int verdict = need ? -2 : -1;  // -2: still searching
+  uint32_t P = 0;                // processed cells
+  while (ballot(verdict == -2)) {
+    const bool run = verdict == -2;
+    const uint32_t lvl = F[0] | F[1] | F[2] | F[3];
+    if (run && n_classes() == 1) {
+      verdict = 1;
+      P = V & ~lvl;
+    }
+    const bool esc = rowbits(ballot((lvl & E) != 0u), row) != 0u;
+    if (verdict == -2 && esc) verdict = -3;  // escaped: caller falls back
+    const bool go = verdict == -2;
+    uint32_t D[4], nw = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      D[d] = ((am4 >> d) & 1u) ? dilate_row(F[d]) & A : 0u;
+      nw |= D[d];
+    }
+    nw &= ~V;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 4; ++j) {
+        const bool cand = go && ((am4 >> i) & 1u) && ((am4 >> j) & 1u) && !((M >> (4 * i + j)) & 1u);
+        if (rowbits(ballot(cand && (D[i] & (F[j] | (D[j] & nw))) != 0u), row)) unite(i, j);
+      }
+    uint32_t reach = 0;  // directions with a new cell
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t fd = D[d] & nw;
+      F[d] = go ? fd : F[d];
+      reach |= rowbits(ballot(fd != 0u), row) ? (1u << d) : 0u;
+    }
+    if (go) {
+      P = V;
+      if (n_classes() == 1) {
+        verdict = 1;
+      } else {
+        bool closed = false;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          closed |= ((am4 >> d) & 1u) && (reach & (M >> (4 * d)) & 15u) == 0u;
+        if (closed)
+          verdict = 0;
+        else
+          V |= nw;
+      }
+    }
+  }
+  if (verdict < 0) return -1;
+  // counters over the processed cells: degree = on-grid 4-neighbours
+  const uint32_t pc = (uint32_t)__popc(P);
+  uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
+  if (c0 <= 0) dg -= (P >> (-c0)) & 1u;          // column 0
+  if (hi_n <= 32) dg -= (P >> (hi_n - 1)) & 1u;  // column W - 1
+  nodes = row_sum(pc);
+  degs = row_sum(dg);
+  return verdict;
+}
+
 // 4-bit scratch field x := 0 (atomic on the shared word)
 __device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
   __atomic_fetch_and(PK<4>::word(scr, x), ~(15u << PK<4>::shift(x)), __ATOMIC_RELAXED);
@@ -402,7 +528,12 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
 
 // FULL = false: the lean instantiation for the common configuration (cut_accept, no
 // spatial maps), which then costs no registers for the optional features.
-template <int LB, int MODE, int PER, bool FULL>
+// BIG = true: grids of more than 256 weight groups (n > 16,384, up to 65,536 nodes: C5's
+// 200x200): selection gets a third level — u16 sums of supergroups of 16 groups (1,024
+// nodes) are scanned first (PER per lane), then the 16 group sums of the chosen supergroup
+// (one per lane), then the 64 nodes of the group — and labels take 3 bits when k <= 8,
+// so that two waves (eight 40,000-node chains) fit one CU's LDS.
+template <int LB, int MODE, int PER, bool FULL, bool BIG>
 __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
   extern __shared__ __align__(16) uint8_t smem[];
@@ -420,11 +551,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   // this row's chain slot (after a 16-B guard: lab_window may read the word before a slot)
   LDS uint8_t* const lab = sm + LDS_GUARD + (wv * 4 + row) * p.slot_stride;
   LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);  // u16 pairs
+  // BIG: supergroup sums (u16 pairs, the level-1 array); otherwise level 1 reads gsum
+  LDS uint32_t* const ssum = reinterpret_cast<LDS uint32_t*>(lab + p.off_ssum);
+  LDS uint32_t* const lvl1 = BIG ? ssum : gsum;
   LDS uint8_t* const scr = sm + p.off_scr;                                        // shared
   LDS uint32_t* const list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list16);  // shared
   GLB uint32_t* const spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)n);
   const uint32_t key0 = (uint32_t)p.seed, key1 = (uint32_t)(p.seed >> 32);
   const int GW = (G + 1) >> 1;  // u16-pair words of group sums
+  const int SG = (G + 15) >> 4;  // BIG: supergroups of 16 groups
   const bool maps_on = FULL && p.m_acc != nullptr;
   // population bounds as int32 (the host routes graphs with total population >= 2^31 to
   // the one-chain-per-wave kernel); clamped so comparisons keep their meaning
@@ -541,9 +676,30 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         }
         if (q == 0 && has) gsum[t2] = tot[0] | (tot[1] << 16);
       }
-      // zero padding up to 16 lanes x PER/2 words: level 1 reads every word unmasked
-      for (int t2 = GW + q; t2 < 8 * PER; t2 += ROW)
-        if (has) gsum[t2] = 0u;
+      if constexpr (BIG) {
+        // group sums zero-padded to whole supergroups (level 2 reads 16 per supergroup)
+        for (int t2 = GW + q; t2 < SG * 8; t2 += ROW)
+          if (has) gsum[t2] = 0u;
+        lds_order();
+        // supergroup sums, two per word, zero past SG: level 1 reads every word unmasked
+        for (int w2 = q; w2 < 8 * PER; w2 += ROW) {
+          uint32_t s2[2] = {0u, 0u};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int sg = 2 * w2 + h;
+            if (sg < SG)
+              for (int i = 0; i < 8; ++i) {
+                const uint32_t g2 = gsum[sg * 8 + i];
+                s2[h] += (g2 & 0xFFFFu) + (g2 >> 16);
+              }
+          }
+          if (has) ssum[w2] = s2[0] | (s2[1] << 16);
+        }
+      } else {
+        // zero padding up to 16 lanes x PER/2 words: level 1 reads every word unmasked
+        for (int t2 = GW + q; t2 < 8 * PER; t2 += ROW)
+          if (has) gsum[t2] = 0u;
+      }
       cut = (int32_t)(row_sum(cut2) / 2);
       bnodes = (int32_t)row_sum(bn);
       npairs = (int32_t)row_sum(np);
@@ -649,7 +805,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
 #pragma unroll
       for (int t = 0; t < PER / 2; ++t) {
         const int wi = q * (PER / 2) + t;
-        const uint32_t w2 = gsum[wi];  // words past GW are zero padding
+        const uint32_t w2 = lvl1[wi];  // words past GW (SG) are zero padding
         gs[2 * t] = w2 & 0xFFFFu;
         gs[2 * t + 1] = w2 >> 16;
 #ifdef FW_VAR_DOT2
@@ -675,8 +831,26 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const int tf = min((int)tfu, PER - 1);
       // pack (group, remaining rank) into one row broadcast
       const uint32_t pk1 = row_pick(((uint32_t)(q * PER + tf) << 16) | ((rl - before) & 0xFFFFu), Lw, q);
-      const int gi = min((int)(pk1 >> 16), G - 1);
-      const uint32_t r1 = pk1 & 0xFFFFu;
+      int gi;
+      uint32_t r1;
+      uint32_t rbg = 1u;
+      if constexpr (BIG) {
+        // level 1.5: the 16 group sums of supergroup sgi, one per row-lane
+        const int sgi = min((int)(pk1 >> 16), SG - 1);
+        const uint32_t r1s = pk1 & 0xFFFFu;
+        const uint32_t g2 = gsum[sgi * 8 + (q >> 1)];
+        const uint32_t gv = (q & 1) ? (g2 >> 16) : (g2 & 0xFFFFu);
+        const uint32_t incg = row_scan(gv);
+        rbg = rowbits(ballot(incg > r1s), row);
+        const int Lg = __ffs(rbg) - 1;
+        const uint32_t pkg =
+            row_pick(((uint32_t)(sgi * 16 + q) << 16) | ((r1s - (incg - gv)) & 0xFFFFu), Lg, q);
+        gi = min((int)(pkg >> 16), G - 1);
+        r1 = pkg & 0xFFFFu;
+      } else {
+        gi = min((int)(pk1 >> 16), G - 1);
+        r1 = pk1 & 0xFFFFu;
+      }
 
       STAMP(1);  // level 1
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
@@ -698,8 +872,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const uint32_t pk2 = row_pick(((uint32_t)(q * 4 + t2) << 16) | ((r2 - bef2) & 0xFFFFu), L2, q);
       const int v = min(gi * 64 + (int)(pk2 >> 16), n - 1);
       const uint32_t j = pk2 & 0xFFFFu;
-      if (act && (rb1 == 0 || rb2 == 0)) stuck = 2;  // inconsistent state: flag, stop chain
-      const bool go = act && rb1 != 0 && rb2 != 0;
+      if (act && (rb1 == 0 || rb2 == 0 || rbg == 0)) stuck = 2;  // inconsistent: flag, stop
+      const bool go = act && rb1 != 0 && rb2 != 0 && rbg != 0;
 
       STAMP(2);  // level 2
       // ---- v's neighbourhood: row-lane roles 0 v, 1 up, 2 left, 3 right, 4 down,
@@ -839,6 +1013,22 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         }
       }
       STAMP(7);  // ring + 7x7 window
+      // large grids (C5: an exact search on a quarter of the steps): every row's search at
+      // once in a 16x32 window first; small grids search rarely (C3: 1%) and keep their
+      // registers for occupancy
+      if (BIG && !p.no_bb && !p.no_rowbb && ballot(need)) {
+        uint32_t bn16 = 0, bd16 = 0;
+        const int vb = grid_race_bb_row<LB>(lab, n, W, H, q, row, need, vr, vc, a, amb,
+                                            (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)),
+                                            bn16, bd16);
+        if (need && vb >= 0) {
+          contig = vb == 1;
+          need = false;
+          n_bfs += 1;
+          n_bfsn += bn16;
+          n_bfsd += bd16;
+        }
+      }
       uint64_t rows_need = ballot(q == 0 && need);
       bool locked = false;
       while (rows_need) {  // wave-cooperative exact search, one chain slot at a time
@@ -850,8 +1040,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         const uint32_t lk = rdl((uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)), L0);
         uint64_t bn = 0, bd = 0;
         int verdict = -1;
-        if (LB == 2 && !p.no_bb)  // bitboard form first; the list search past its window
-          verdict = grid_race_bb<2>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, n, W, H,
+        if (!p.no_bb)  // bitboard form first; the list search past its window
+          verdict = grid_race_bb<LB>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, n, W, H,
                                     lane, rdl(vr, L0), rdl(vc, L0), aa, am4, lk, bn, bd);
         if (verdict >= 0) {
           if (row == rr) {
@@ -986,8 +1176,10 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (q == 0) P::axor(lab, v, a ^ d);
         // u16 group sum inside its u32 pair: a wrapping 32-bit add of the shifted
         // delta changes only that half (both halves stay in [0, 65535])
-        if (mine && wn != wo)
+        if (mine && wn != wo) {
           lds_add(gsum + (h.x >> 7), (wn - wo) << (16 * ((h.x >> 6) & 1)));
+          if (BIG) lds_add(ssum + (h.x >> 11), (wn - wo) << (16 * ((h.x >> 10) & 1)));
+        }
       }
       lds_order();
       // lanes 0..4 hold the changes: a 3-step row_shr scan leaves their sum on lane 4
@@ -1066,16 +1258,31 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   STAMP_FLUSH
 }
 
-// group sums per lane (PER) for G groups
+// group sums per lane (PER) for G groups; BIG: supergroup sums per lane for G groups
 int per16(int G) { return G <= 16 * 2 ? 2 : G <= 16 * 4 ? 4 : G <= 16 * 10 ? 10 : 16; }
+int per16_big(int G) { return (G + 15) / 16 <= 32 ? 2 : 4; }
+bool is_big(int G) { return G > 16 * 16; }
 
 template <int LB, int MODE, bool FULL>
 void* pick16(int G) {
-  switch (per16(G)) {
-    case 2: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL>);
-    case 4: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL>);
-    case 10: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL>);
-    default: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL>);
+  if (is_big(G)) {
+    if constexpr (LB == 4) {
+      return nullptr;  // large grids take 2- or 3-bit labels
+    } else {
+      return per16_big(G) == 2
+                 ? reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL, true>)
+                 : reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL, true>);
+    }
+  }
+  if constexpr (LB == 3) {
+    return nullptr;  // small grids keep 2- or 4-bit labels
+  } else {
+    switch (per16(G)) {
+      case 2: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL, false>);
+      case 4: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL, false>);
+      case 10: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL, false>);
+      default: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL, false>);
+    }
   }
 }
 
@@ -1084,6 +1291,8 @@ void* pick16_mode(const FwRunParams& p) {
   const bool cut = p.mode == FW_PROPOSE_CUTEDGE;
   if (p.lb == 2)
     return cut ? pick16<2, FW_PROPOSE_CUTEDGE, FULL>(p.G) : pick16<2, FW_PROPOSE_PAIRS, FULL>(p.G);
+  if (p.lb == 3)
+    return cut ? pick16<3, FW_PROPOSE_CUTEDGE, FULL>(p.G) : pick16<3, FW_PROPOSE_PAIRS, FULL>(p.G);
   return cut ? pick16<4, FW_PROPOSE_CUTEDGE, FULL>(p.G) : pick16<4, FW_PROPOSE_PAIRS, FULL>(p.G);
 }
 
@@ -1103,11 +1312,24 @@ extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+// Largest k the large-grid plan takes.  With k <= 4 (2-bit labels, 12 chains per CU) it
+// runs 200x200 chains 2.6x faster than the one-chain-per-wave kernel; with 5 <= k <= 8
+// (3-bit labels) only 8 chains fit a CU in two waves, and C5's search-heavy low-base
+// chains ran 10% slower than on the one-chain-per-wave kernel (profiles/r02/ab_big.jsonl),
+// so those stay there unless FLIPWALK_BIG_K8=1.
+int big_max_k() {
+  const char* e = getenv("FLIPWALK_BIG_K8");
+  return e && e[0] == '1' ? 8 : 4;
+}
+
 bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop) {
   // gw >= 4: four consecutive nodes span at most one row wrap (weights4_swar masks);
-  // populations are held as int32
-  return gw >= 4 && maxdeg == 4 && G <= 16 * 16 && k <= 15 && total_pop < (1ll << 31) - 1;
+  // populations are held as int32; large grids (> 256 groups, <= 1,024) need k <= 8
+  return gw >= 4 && maxdeg == 4 && total_pop < (1ll << 31) - 1 &&
+         ((G <= 16 * 16 && k <= 15) || (G <= 64 * 16 && k <= big_max_k()));
 }
+
+int fw_grid16_lb(int G, int k) { return k <= 4 ? 2 : (is_big(G) ? 3 : 4); }
 
 void* fw_grid16_fn(const FwRunParams& p) {
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
@@ -1120,14 +1342,21 @@ void* fw_grid16_fn(const FwRunParams& p) {
 // 4-bit search scratch and visit list.  Picks the waves per workgroup (1..4) that keep
 // the most chains resident per CU (ties: fewer waves).
 int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
-  const int slot = round16i(p.lab_bytes) + 4 * 8 * per16(p.G);  // + u16 sums, 16 x PER
+  // slot: labels | u16 group sums (16 x PER per row; BIG: padded to whole supergroups) |
+  // BIG: u16 supergroup sums (16 x PER)
+  const bool big = is_big(p.G);
+  const int gbytes = big ? round16i((p.G + 15) / 16 * 16 * 2) : 4 * 8 * per16(p.G);
+  const int sbytes = big ? 4 * 8 * per16_big(p.G) : 0;
+  const int slot = round16i(p.lab_bytes) + gbytes + sbytes;
   int stride = slot;
   while (stride % 128 != 16) stride += 16;
   p.slot_stride = stride;
   p.off_gsum = round16i(p.lab_bytes);
+  p.off_ssum = p.off_gsum + gbytes;
   p.scr_bytes = round16i((p.g.n + 1) / 2 + 8);
   if (p.qcap16 <= 0) p.qcap16 = 384;
   void* fn = fw_grid16_fn(p);
+  if (!fn) return -1;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
   int best_nw = 0, best_chains = 0, best_lds = 0;
@@ -1153,6 +1382,11 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   p.lds16 = best_lds;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, best_lds) != hipSuccess)
     return -1;
+  const char* verbose = getenv("FLIPWALK_VERBOSE");
+  if (verbose && verbose[0] == '1')
+    fprintf(stderr, "flipwalk: grid kernel %s, %d-bit labels, LDS %d B per workgroup of %d waves, "
+            "%d chains per CU\n", is_big(p.G) ? "large-grid plan" : "small-grid plan", p.lb,
+            best_lds, best_nw, best_chains);
   const long long per_wg = 4LL * best_nw;
   long long gsz = (long long)(best_chains / per_wg) * prop.multiProcessorCount;
   const long long need = (p.n_chains + per_wg - 1) / per_wg;
@@ -1164,9 +1398,9 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
 int fw_grid16_launch(const FwRunParams& p, int grid, void* stream) {
   void* args[] = {const_cast<FwRunParams*>(&p)};
   void* fn = fw_grid16_fn(p);  // the lean or the FULL instantiation (same LDS plan)
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds16) != hipSuccess)
-    return -1;
-  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * p.nw), args,
-                                 (size_t)p.lds16, (hipStream_t)stream);
-  return e == hipSuccess ? 0 : -1;
+  if (!fn) return (int)hipErrorInvalidDeviceFunction;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds16);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipLaunchKernel(fn, dim3(grid), dim3(64 * p.nw), args, (size_t)p.lds16,
+                              (hipStream_t)stream);
 }

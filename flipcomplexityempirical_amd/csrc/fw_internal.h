@@ -62,6 +62,7 @@ struct FwRunParams {
   // LDS layout (bytes from the dynamic shared base)
   int32_t lab_bytes;           // packed label bytes (multiple of 16)
   int32_t off_gsum, off_list, lds_bytes;
+  int32_t off_ssum;            // grid kernel, large grids: supergroup sums in the slot
   int32_t lb;                  // label bits per node (2, 4 or 8)
   int32_t use16;               // 1: launch the four-chains-per-wave grid kernel
   // grid kernel LDS plan (fw_grid16_plan): 4*nw chain slots, shared scratch and list
@@ -70,6 +71,7 @@ struct FwRunParams {
   int32_t off_scr, scr_bytes;  // 4-bit search scratch
   int32_t off_list16, qcap16;  // shared visit list
   int32_t no_bb;               // 1: exact searches skip the bitboard form (tests)
+  int32_t no_rowbb;            // 1: large grids skip the row-parallel bitboard form (A/B)
   int32_t wpe5;                // 1: the 5-waves-per-SIMD chain-kernel instantiation
   int32_t lds16;               // dynamic LDS bytes per workgroup
   // spatial observables (nullptr: off).  Per chain c: acc [E] (int64: sum of -t when an
@@ -143,6 +145,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);
 int fw_run_gsum_words(int G);
 // fw_grid16.hip
 bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop);
+int fw_grid16_lb(int G, int k);
 void* fw_grid16_fn(const FwRunParams& p);
 int fw_grid16_plan(FwRunParams& p, int device, int* grid);
 int fw_grid16_launch(const FwRunParams& p, int grid, void* stream);

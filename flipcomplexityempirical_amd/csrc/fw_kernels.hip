@@ -418,8 +418,9 @@ __global__ __launch_bounds__(64) void fw_eval_kernel(FwEvalParams p) {
 
 // ---------------------------------------------------------------- spatial-observable maps
 __device__ __forceinline__ uint32_t glabel(const uint8_t* lab, int lb, int x) {
-  const int bit = x * lb;
-  return (uint32_t)(lab[bit >> 3] >> (bit & 7)) & ((1u << lb) - 1u);
+  const int bit = x * lb;  // a 3-bit field may straddle two bytes (the region is padded)
+  const uint32_t v = (uint32_t)lab[bit >> 3] | ((uint32_t)lab[(bit >> 3) + 1] << 8);
+  return (v >> (bit & 7)) & ((1u << lb) - 1u);
 }
 
 // part_sum := label value of the initial plan (grid_chain_sec11.py:219); pending runs none
@@ -588,11 +589,11 @@ int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   if (p.use16) return fw_grid16_launch(p, grid, stream);
   void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0);
   // handles of different graphs share instantiations: set this handle's LDS size
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) != hipSuccess)
-    return -1;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
+  if (e != hipSuccess) return (int)e;
   void* args[] = {const_cast<FwRunParams*>(&p)};
-  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes, (hipStream_t)stream);
-  return e == hipSuccess ? 0 : -1;
+  return (int)hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes,
+                              (hipStream_t)stream);
 }
 
 // flagged nodes per district of every chain's current plan (FW_ACCEPT_BOUNDARY)
@@ -606,21 +607,27 @@ __global__ void fw_bcnt_init_kernel(FwRunParams p, int lb) {
   }
 }
 
+// Launchers return the hipError_t of the launch itself (0 = hipSuccess).
 int fw_launch_bcnt_init(const FwRunParams& p, void* stream) {
-  hipLaunchKernelGGL(fw_bcnt_init_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, p, p.lb);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  int lb = p.lb;
+  void* args[] = {const_cast<FwRunParams*>(&p), &lb};
+  return (int)hipLaunchKernel(reinterpret_cast<void*>(&fw_bcnt_init_kernel), dim3(2048), dim3(256),
+                              args, 0, (hipStream_t)stream);
 }
 
 int fw_launch_map_init(const FwRunParams& p, void* stream) {
-  hipLaunchKernelGGL(fw_map_init_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, p, p.lb);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  int lb = p.lb;
+  void* args[] = {const_cast<FwRunParams*>(&p), &lb};
+  return (int)hipLaunchKernel(reinterpret_cast<void*>(&fw_map_init_kernel), dim3(2048), dim3(256),
+                              args, 0, (hipStream_t)stream);
 }
 
 int fw_launch_map_read(const FwMapRead& m, void* stream) {
   const int M = m.what == FW_MAP_CUT_TIMES ? m.E : m.n;
   const int blocks = (M + 255) / 256;
-  hipLaunchKernelGGL(fw_map_read_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, m);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  void* args[] = {const_cast<FwMapRead*>(&m)};
+  return (int)hipLaunchKernel(reinterpret_cast<void*>(&fw_map_read_kernel), dim3(blocks),
+                              dim3(256), args, 0, (hipStream_t)stream);
 }
 
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream) {
@@ -631,11 +638,9 @@ int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream) {
   else
     fn = p.g.gw > 0 ? reinterpret_cast<void*>(&fw_eval_kernel<8, true>)
                     : reinterpret_cast<void*>(&fw_eval_kernel<8, false>);
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
-      hipSuccess)
-    return -1;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
+  if (e != hipSuccess) return (int)e;
   void* args[] = {const_cast<FwEvalParams*>(&p)};
-  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes,
-                                 (hipStream_t)stream);
-  return e == hipSuccess ? 0 : -1;
+  return (int)hipLaunchKernel(fn, dim3(grid), dim3(64), args, (size_t)p.lds_bytes,
+                              (hipStream_t)stream);
 }

@@ -30,7 +30,8 @@ def ladder(n_bases: int = 64, lo: float = 0.1, hi: float = 10.0) -> np.ndarray:
     return np.geomspace(lo, hi, n_bases)
 
 
-def ladder_base_index(cid, n_bases: int = 64, n_gpus_hint: int = 8) -> np.ndarray:
+def ladder_base_index(cid, n_bases: int = 64, n_gpus_hint: int = 8,
+                      interleave: bool = True) -> np.ndarray:
     """Ladder index of global chain id(s) ``cid``: base group b = cid // 1024 runs ladder
     entry (b % 8) * 8 + b // 8.  Every 8,192-id block (one GPU's shard at 8 GPUs) thus
     holds 8 whole base groups spread over the ladder (entries r, r+8, ..., r+56) instead
@@ -40,6 +41,8 @@ def ladder_base_index(cid, n_bases: int = 64, n_gpus_hint: int = 8) -> np.ndarra
     b = np.asarray(cid, np.int64) // LADDER_GROUP
     per = n_bases // n_gpus_hint
     b = b % n_bases
+    if not interleave:  # round 1's assignment: adjacent groups, ladder entry b
+        return b
     return (b % per) * n_gpus_hint + b // per
 
 
@@ -55,16 +58,18 @@ class Workload:
     base: Optional[float]   # shared Metropolis base, or None for the C5 ladder
     desc: str
 
+    interleave: bool = True  # C5: ladder_base_index's spread of base groups over shards
+
     def bases(self, lo: int, hi: int):
         """Base(s) of global chain ids [lo, hi): a float, or a per-chain array (ladder)."""
         if self.base is not None:
             return self.base
-        return ladder()[ladder_base_index(np.arange(lo, hi))]
+        return ladder()[ladder_base_index(np.arange(lo, hi), interleave=self.interleave)]
 
     def base_desc(self, lo: int, hi: int) -> str:
         if self.base is not None:
             return f"base {self.base:.9g}"
-        idx = np.unique(ladder_base_index(np.arange(lo, hi)))
+        idx = np.unique(ladder_base_index(np.arange(lo, hi), interleave=self.interleave))
         return (f"{len(idx)} ladder bases x {LADDER_GROUP} chains "
                 f"({', '.join(f'{b:.3g}' for b in ladder()[idx][:8])}"
                 f"{', ...' if len(idx) > 8 else ''})")

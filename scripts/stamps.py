@@ -10,15 +10,18 @@ import numpy as np  # noqa: E402
 
 from flipcomplexityempirical_amd import _lib  # noqa: E402
 from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bounds  # noqa: E402
-from flipcomplexityempirical_amd.graph import block_seed, grid_graph  # noqa: E402
 
 L = _lib.load()
 L.fw_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-g = grid_graph(n, n)
+# usage: stamps.py [config] [chains]   (config c3 default; c5 = the 64-base ladder workload)
+from flipcomplexityempirical_amd.workloads import workload  # noqa: E402
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+w = workload(cfg)
+nch = int(sys.argv[2]) if len(sys.argv) > 2 else w.chains
+g = w.graph
 dg = DeviceGraph(g)
-ch = Chains(dg, 65536, 4, block_seed(n, n, 2, 2), proposal="pairs",
-            pop_bounds=population_bounds(n * n, 4, 0.05), base=2.63815853, seed=0)
+ch = Chains(dg, nch, w.k, w.init, proposal=w.proposal,
+            pop_bounds=population_bounds(g.total_pop, w.k, w.percent), base=w.bases(0, nch), seed=0)
 ch.run(1000)
 ch.run(1000)
 buf = np.zeros(16, np.uint64)

@@ -420,3 +420,102 @@ def test_checkpoint_resume_bit_exact(gpu_lib, name, path, monkeypatch, tmp_path)
     # the resumed run is also the oracle's uninterrupted 700-step run
     _, ost = oracle_chains(case, 71, range(9, 21), [700])[:2]
     assert_stats_equal(ch2.stats(), ost)
+
+
+BIG_CASES = [  # (h, w, k, seed blocks or bands, proposal, base, env)
+    ("big132_k8_pairs", 132, 132, 8, (2, 4), "pairs", 0.5, {"FLIPWALK_BIG_K8": "1"}),
+    ("big132_k8_cut", 132, 132, 8, (2, 4), "cutedge", 1.5, {"FLIPWALK_BIG_K8": "1"}),
+    ("big132_k8_norow", 132, 132, 8, (2, 4), "pairs", 0.3,
+     {"FLIPWALK_BIG_K8": "1", "FLIPWALK_NO_ROWBB": "1"}),
+    ("big130x135_k4", 130, 135, 4, "band", "pairs", 0.5, {}),
+    ("big200_k4_cut", 200, 200, 4, (2, 2), "cutedge", 0.8, {}),
+    ("big200_k2_cold", 200, 200, 2, "band", "bi", 0.2, {}),
+    ("big132_k6_list", 132, 132, 6, "band", "pairs", 0.3,
+     {"FLIPWALK_BIG_K8": "1", "FLIPWALK_NO_BITBOARD": "1"}),
+    ("big132_k3_spill", 132, 132, 3, "band", "pairs", 0.3,
+     {"FLIPWALK_NO_BITBOARD": "1", "FLIPWALK_LIST_CAP": "2"}),
+    ("big256_k8", 256, 256, 8, (2, 4), "pairs", 1.0, {"FLIPWALK_BIG_K8": "1"}),
+    ("big256_k4", 256, 256, 4, (2, 2), "pairs", 0.4, {}),
+]
+
+
+@pytest.mark.parametrize("name,h,w,k,seedspec,proposal,base,env", BIG_CASES,
+                         ids=[c[0] for c in BIG_CASES])
+def test_big_grid_kernel_bit_exact(gpu_lib, name, h, w, k, seedspec, proposal, base, env,
+                                   monkeypatch):
+    """The grid kernel's large-grid plan (more than 256 weight groups: supergroup level,
+    3-bit labels for 5 <= k <= 8, 2-bit for k <= 4), 37 chains over several waves and
+    workgroups, two launches, against the oracle: plans, every counter, the fp64 sum,
+    histograms.  Also the list search (bitboard off) with the shared scratch, its HBM spill,
+    widths that are not multiples of 4 and the 65,536-node maximum."""
+    from flipcomplexityempirical_amd.chain import PROPOSALS, metropolis_table, population_bounds
+    from flipcomplexityempirical_amd.graph import band_seed, block_seed, grid_graph
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    for kk, vv in env.items():
+        monkeypatch.setenv(kk, vv)
+    g = grid_graph(h, w)
+    init = band_seed(h, w, k) if seedspec == "band" else block_seed(h, w, *seedspec)
+    pct = 0.3 if seedspec == "band" else 0.05
+    bounds = population_bounds(g.total_pop, k, pct)
+    n_chains, seed, id0, steps = 37, 12, 100, [400, 250]
+    dg = DeviceGraph(g)
+    ch = Chains(dg, n_chains, k, init, proposal=proposal, pop_bounds=bounds, base=base, seed=seed,
+                chain_id0=id0)
+    for s in steps:
+        ch.run(s)
+    labs, st = ch.labels(), ch.stats()
+    thr = metropolis_table(base, 4)
+    hc = np.zeros(g.n_edges + 1, np.uint64)
+    hb = np.zeros(g.n + 1, np.uint64)
+    for i in range(n_chains):
+        lab, ost = init.copy(), O.new_stats(1)
+        for s in steps:
+            lab, ost, _, _ = O.run_chain(g, lab, k, PROPOSALS[proposal], *bounds, thr, seed,
+                                         id0 + i, s, stats=ost, hist_cut=hc, hist_b=hb)
+        assert np.array_equal(labs[i], lab), (name, i)
+        assert_stats_equal(st[i:i + 1], ost)
+    assert np.array_equal(ch.hist_cut(), hc) and np.array_equal(ch.hist_b(), hb)
+    assert st["bfs_runs"].sum() > 0
+
+
+@pytest.mark.parametrize("feature", ["maps", "ring", "bratio"])
+def test_big_grid_full_instantiation(gpu_lib, feature, monkeypatch):
+    """The large-grid plan's FULL instantiation (spatial maps, the ring observable, the
+    |B'|/|B| accept rule) against the oracle on a 150x150 k=2 grid."""
+    from flipcomplexityempirical_amd import shape
+    from flipcomplexityempirical_amd.chain import (annealing_table, metropolis_table,
+                                                   population_bounds)
+    from flipcomplexityempirical_amd.graph import grid_graph, stripe_seed
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    n = 150
+    g = grid_graph(n, n)
+    init = stripe_seed(n, n)
+    bounds = population_bounds(g.total_pop, 2, 0.1)
+    thr = annealing_table(0.9, 1, 4) if feature == "bratio" else metropolis_table(0.7, 4)
+    dg = DeviceGraph(g)
+    ch = Chains(dg, 6, 2, init, proposal="bi", pop_bounds=bounds, seed=3, chain_id0=0, thr=thr)
+    ru, rw = shape.ring_edges(g, shape.grid_on_ring(n, n))
+    if feature == "maps":
+        ch.enable_maps([-1, 1])
+    elif feature == "ring":
+        ch.enable_ring(ru, rw)
+    else:
+        ch.set_accept("bratio")
+    for s in (300, 200):
+        ch.run(s)
+    labs, st = ch.labels(), ch.stats()
+    ring = O.Ring(ru, rw)
+    for i in range(6):
+        lab, ost = init.copy(), O.new_stats(1)
+        maps = O.Maps(g, init, np.array([-1, 1], np.int64)) if feature == "maps" else None
+        for s in (300, 200):
+            lab, ost, _, _ = O.run_chain(g, lab, 2, 0, *bounds, thr, 3, i, s, stats=ost,
+                                         maps=maps, ring=ring if feature == "ring" else None,
+                                         accept_rule=1 if feature == "bratio" else 0)
+        assert np.array_equal(labs[i], lab), i
+        assert_stats_equal(st[i:i + 1], ost)
+        if feature == "maps":
+            assert np.array_equal(ch.read_map("cut_times", (i, i + 1))[0], maps.cut_times)
+            assert np.array_equal(ch.read_map("num_flips", (i, i + 1))[0], maps.num_flips)
+    if feature == "ring":
+        assert np.array_equal(ch.hist_ring(), ring.hist)
