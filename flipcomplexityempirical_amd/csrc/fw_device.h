@@ -512,6 +512,9 @@ struct Ctx {
   int lane;
   bool bb;  // grids: exact searches try the bitboard form first
   int my_dr, my_dc;
+#ifdef FW_STAMPS
+  uint32_t n_win = 0, n_bbs = 0, n_list = 0;  // contiguity checks by the path that decided
+#endif
 
   __device__ void init_roles() {
     lane = lane_id();
@@ -942,6 +945,9 @@ struct Ctx {
         const uint64_t b48 = ballot(in) & ((1ull << 48) - 1ull);
         const uint64_t A = (b48 & ((1ull << 24) - 1ull)) | ((b48 >> 24) << 25);
         const int wv = window_verdict(A);
+#ifdef FW_STAMPS
+        n_win += 1;
+#endif
         if (wv >= 0) return wv == 1;
       }
       if (bb) {  // bitboard search first; the list search past its window
@@ -951,6 +957,9 @@ struct Ctx {
                                         (uint32_t)(am >> 1) & 15u,
                                         (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)),
                                         bfs_nodes, bfs_deg);
+#ifdef FW_STAMPS
+        n_bbs += 1;
+#endif
         if (wv >= 0) {
           bfs_runs += 1;
           return wv == 1;
@@ -963,6 +972,9 @@ struct Ctx {
       if (lWN) merge(sx(2), sx(1));
     }
     bfs_runs += 1;
+#ifdef FW_STAMPS
+    n_list += 1;
+#endif
     // sources (a-labelled neighbours, CSR order) compacted into lanes 0..m-1
     int src = -1;
     uint64_t mm = am;

@@ -50,6 +50,22 @@ __device__ unsigned long long g_stamps[16];
 #define STAMP_FLUSH
 #endif
 
+#include <cstddef>
+
+// the write-back stores the stats record as 8-byte pairs in declaration order
+static_assert(sizeof(fw_chain_stats) == 136, "fw_chain_stats layout");
+static_assert(offsetof(fw_chain_stats, yields) == 88 && offsetof(fw_chain_stats, sum_invb) == 112 &&
+                  offsetof(fw_chain_stats, cut) == 120 && offsetof(fw_chain_stats, npairs) == 128,
+              "fw_chain_stats layout");
+
+// FW_VAR_NOHIST (diagnostic variant only): histogram flushes dropped, to size their write
+// traffic in a PMC pass
+#ifdef FW_VAR_NOHIST
+#define HIST_ADD(ptr, v) ((void)(ptr), (void)(v))
+#else
+#define HIST_ADD(ptr, v) atomicAdd(ptr, v)
+#endif
+
 namespace {
 
 constexpr int ROW = 16;
@@ -740,8 +756,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       sum_invb += invb;
       int ic = cut - base_c;
       if (ic < 0 || ic >= 2 * ROW) {
-        if (hc0) atomicAdd(p.hist_cut + base_c + q, (unsigned long long)hc0);
-        if (hc1) atomicAdd(p.hist_cut + base_c + ROW + q, (unsigned long long)hc1);
+        if (hc0) HIST_ADD(p.hist_cut + base_c + q, (unsigned long long)hc0);
+        if (hc1) HIST_ADD(p.hist_cut + base_c + ROW + q, (unsigned long long)hc1);
         hc0 = hc1 = 0;
         base_c = max(0, cut - ROW);
         ic = cut - base_c;
@@ -750,8 +766,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       hc1 += ic == q + ROW;
       int ib = bnodes - base_b;
       if (ib < 0 || ib >= 2 * ROW) {
-        if (hb0) atomicAdd(p.hist_b + base_b + q, (unsigned long long)hb0);
-        if (hb1) atomicAdd(p.hist_b + base_b + ROW + q, (unsigned long long)hb1);
+        if (hb0) HIST_ADD(p.hist_b + base_b + q, (unsigned long long)hb0);
+        if (hb1) HIST_ADD(p.hist_b + base_b + ROW + q, (unsigned long long)hb1);
         hb0 = hb1 = 0;
         base_b = max(0, bnodes - ROW);
         ib = bnodes - base_b;
@@ -1220,10 +1236,10 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     STAMP(6);  // loop exit
     // ---- write back
     if (has) {
-      if (hc0) atomicAdd(p.hist_cut + base_c + q, (unsigned long long)hc0);
-      if (hc1) atomicAdd(p.hist_cut + base_c + ROW + q, (unsigned long long)hc1);
-      if (hb0) atomicAdd(p.hist_b + base_b + q, (unsigned long long)hb0);
-      if (hb1) atomicAdd(p.hist_b + base_b + ROW + q, (unsigned long long)hb1);
+      if (hc0) HIST_ADD(p.hist_cut + base_c + q, (unsigned long long)hc0);
+      if (hc1) HIST_ADD(p.hist_cut + base_c + ROW + q, (unsigned long long)hc1);
+      if (hb0) HIST_ADD(p.hist_b + base_b + q, (unsigned long long)hb0);
+      if (hb1) HIST_ADD(p.hist_b + base_b + ROW + q, (unsigned long long)hb1);
       if (FULL && RN && q == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
@@ -1231,26 +1247,35 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (q < k) p.pops[(size_t)c * k + q] = (int64_t)pops;
       if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
       if (q == 0 && maps_on) pend_store(p, c, pend);
-      if (q == 0) {
-        stp->attempts = att0 + n_att;
-        stp->steps += n_steps;
-        stp->accepts += n_acc;
-        stp->pop_fail += n_popf;
-        stp->contig_fail += n_conf;
-        stp->bfs_runs += n_bfs;
-        stp->bfs_nodes += n_bfsn;
-        stp->bfs_deg += n_bfsd;
-        stp->sum_deg += n_sdeg;
-        stp->acc_deg += n_adeg;
-        stp->n_bchg += n_bchg;
-        stp->yields += (uint64_t)n_steps + (first ? 1u : 0u);
-        stp->sum_cut = sum_cut;
-        stp->sum_bnodes = sum_bnodes;
-        stp->sum_invb = sum_invb;
-        stp->cut = cut;
-        stp->bnodes = bnodes;
-        stp->npairs = npairs;
-        stp->stuck = stuck;
+      // the 136-byte stats record as 16-byte read-modify-writes by row-lanes 0..8 (every
+      // lane of a row holds the row-uniform values): 9 requests instead of 19 4- and 8-byte
+      // ones (no measurable change in time or PMC WRITE_SIZE: profiles/r02/c3)
+      if (q <= 8) {
+        uint64_t* rec = reinterpret_cast<uint64_t*>(stp);
+        const uint64_t o0 = rec[2 * q];
+        const uint64_t o1 = q < 8 ? rec[2 * q + 1] : 0ull;
+        const uint64_t yinc = (uint64_t)n_steps + (first ? 1u : 0u);
+        uint64_t w0, w1;
+        switch (q) {
+          case 0: w0 = att0 + n_att; w1 = o1 + n_steps; break;
+          case 1: w0 = o0 + n_acc; w1 = o1 + n_popf; break;
+          case 2: w0 = o0 + n_conf; w1 = o1 + n_bfs; break;
+          case 3: w0 = o0 + n_bfsn; w1 = o1 + n_bfsd; break;
+          case 4: w0 = o0 + n_sdeg; w1 = o1 + n_adeg; break;
+          case 5: w0 = o0 + n_bchg; w1 = o1 + yinc; break;
+          case 6: w0 = (uint64_t)sum_cut; w1 = (uint64_t)sum_bnodes; break;
+          case 7:
+            w0 = (uint64_t)__double_as_longlong(sum_invb);
+            w1 = (uint64_t)(uint32_t)cut | ((uint64_t)(uint32_t)bnodes << 32);
+            break;
+          default: w0 = (uint64_t)(uint32_t)npairs | ((uint64_t)(uint32_t)stuck << 32); w1 = 0;
+        }
+        if (q < 8) {
+          typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u64x2*>(rec + 2 * q) = u64x2{w0, w1};
+        } else {
+          rec[16] = w0;
+        }
       }
     }
     lds_order();

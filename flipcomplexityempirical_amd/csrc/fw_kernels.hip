@@ -29,6 +29,31 @@
 
 #include "fw_device.h"
 
+#ifdef FW_STAMPS
+// Diagnostic build only (libflipwalk_stamps.so): per-phase s_memtime shares of the
+// one-chain-per-wave kernel (scripts/stamps.py --csr).
+__device__ unsigned long long g_stamps_csr[16];
+#define CSTAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_t0 = 0;
+#define CSTAMP(i)                                             \
+  do {                                                        \
+    __builtin_amdgcn_sched_barrier(0);                        \
+    uint64_t st_t1;                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t1)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                        \
+    if (i >= 0) st_acc[(i) < 0 ? 0 : (i)] += st_t1 - st_t0;   \
+    st_t0 = st_t1;                                            \
+  } while (0)
+#define CSTAMP_COUNT(i, v) st_acc[i] += (uint64_t)(v)
+#define CSTAMP_FLUSH                                          \
+  if (__lane_id() == 0)                                       \
+    for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_stamps_csr[i_], (unsigned long long)st_acc[i_]);
+#else
+#define CSTAMP_DECL
+#define CSTAMP(i)
+#define CSTAMP_COUNT(i, v)
+#define CSTAMP_FLUSH
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------- the chain kernel
@@ -55,6 +80,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const int k = p.k;
   const uint32_t key0 = (uint32_t)p.seed, key1 = (uint32_t)(p.seed >> 32);
   __shared__ int32_t s_chain;
+  CSTAMP_DECL
 
   for (;;) {
     if (lane == 0) s_chain = atomicAdd(p.next_chain, 1);
@@ -180,6 +206,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       Hood h;
       bool valid = false;
       for (;;) {
+        CSTAMP(-1);
         if (retries >= p.max_retries || npairs == 0) {
           stuck = 1;
           break;
@@ -205,7 +232,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         attempts += 1;
         const uint32_t r = scale64(x.x0, x.x1, (uint32_t)npairs);
         uint32_t j = 0;
+        CSTAMP(0);  // draw
         C.template select<MODE, PER>(r, G, v, j);
+        CSTAMP(1);  // select
         v = rfl(v);
         if (v < 0) {  // internal inconsistency: stop this chain, flag it
           stuck = 2;
@@ -245,10 +274,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (pa - pv < p.pop_lo || pb + pv > p.pop_hi) {
           n_popf += 1;
           ++retries;
+          CSTAMP(2);
           continue;
         }
         // ---- contiguity (single_flip_contiguous)
-        if (!C.contiguous(v, a, m, h, am, n_bfs, n_bfsn, n_bfsd)) {
+        CSTAMP(2);  // gather, target, population
+        const bool cg = C.contiguous(v, a, m, h, am, n_bfs, n_bfsn, n_bfsd);
+        CSTAMP(3);  // contiguity
+        if (!cg) {
           n_conf += 1;
           ++retries;
           continue;
@@ -260,6 +293,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       n_steps += 1;
       // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
       uint32_t wo, wn;
+      CSTAMP(-1);
       C.template weights_old_new<MODE>(h, a, d, m, nbd, wo, wn);
       const bool mine = GRID ? lane <= 4 : lane <= dv;
       const int plus = __popcll(ballot(mine && wo == 0 && wn > 0));
@@ -325,7 +359,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           }
         }
       }
+      CSTAMP(4);  // outcome, accept, commit
       observe();
+      CSTAMP(5);  // observe
     }
 
     // ---- write back
@@ -363,6 +399,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     __syncthreads();
   }
+#ifdef FW_STAMPS
+  CSTAMP_COUNT(8, C.n_win);
+  CSTAMP_COUNT(9, C.n_bbs);
+  CSTAMP_COUNT(10, C.n_list);
+#endif
+  CSTAMP_FLUSH
 }
 
 // ---------------------------------------------------------------- per-flip evaluation
@@ -481,6 +523,18 @@ __global__ void fw_map_read_kernel(FwMapRead m) {
 }
 
 }  // namespace
+
+#ifdef FW_STAMPS
+extern "C" int fw_debug_stamps_csr(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_csr), sizeof(unsigned long long) * 16) != hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_csr), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // group sums per lane of the one-chain-per-wave kernel (pick_per) and the LDS words its
 // padded level-1 layout (gsum_slot) takes for G groups

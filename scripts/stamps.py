@@ -26,6 +26,8 @@ ch.run(1000)
 ch.run(1000)
 buf = np.zeros(16, np.uint64)
 L.fw_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), 1)
+L.fw_debug_stamps_csr.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.fw_debug_stamps_csr(buf.ctypes.data_as(ctypes.c_void_p), 1)
 att0 = int(ch.stats()["attempts"].sum())
 for _ in range(3):
     ch.run(1000)
@@ -40,3 +42,17 @@ print(f"7x7 window runs per wave-iter {buf[12] / iters:.3f}, flood iterations pe
 for nm, v in zip(names, buf):
     if v:
         print(f"{nm:16s} {v / tot * 100:6.2f} %  {v / iters:8.1f} clk/wave-iter")
+
+# the one-chain-per-wave kernel's stamps (configurations routed to it, e.g. C4, C5)
+L.fw_debug_stamps_csr.argtypes = [ctypes.c_void_p, ctypes.c_int]
+cb = np.zeros(16, np.uint64)
+L.fw_debug_stamps_csr(cb.ctypes.data_as(ctypes.c_void_p), 0)
+if cb[:6].sum():
+    att = int(st["attempts"].sum()) - att0
+    cn = ["draw", "select", "gather+target+pop", "contiguity", "accept+commit", "observe"]
+    tot = cb[:6].sum()
+    print("one-chain-per-wave kernel, attempts timed:", att)
+    for nm, v in zip(cn, cb[:6]):
+        print(f"{nm:18s} {v / tot * 100:6.2f} %  {v / att:8.1f} clk/attempt")
+    print(f"contiguity decided by: 7x7 window {cb[8] / att:.3f}/attempt, bitboard search "
+          f"{cb[9] / att:.3f}, list search {cb[10] / att:.3f}")
