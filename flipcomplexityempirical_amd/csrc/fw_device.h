@@ -216,6 +216,28 @@ __device__ __forceinline__ int window_verdict(uint64_t A) {
   }
   return verdict;
 }
+// window_verdict with the four source flood fills run side by side in lanes 0..3 (VALU,
+// two dilations per convergence test) instead of one after another on the scalar unit.
+// Fills of sources in one window component are equal and the others disjoint, so the
+// sequential verdict is order-free: 1 if some fill holds every source, else 0 if some
+// fill touches no border, else -1.  Wave-uniform result.
+__device__ __forceinline__ int window_verdict_lanes(uint64_t A, int lane) {
+  const uint64_t C0 = 0x0040810204081ull, C6 = C0 << 6;
+  const uint64_t BORDER = C0 | C6 | 0x7Full | (0x7Full << 42);
+  const uint64_t src = A & ((1ull << 17) | (1ull << 23) | (1ull << 25) | (1ull << 31));
+  const int sb = lane == 0 ? 17 : lane == 1 ? 23 : lane == 2 ? 25 : 31;
+  uint64_t x = lane < 4 ? src & (1ull << sb) : 0ull;
+  for (;;) {
+    const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
+    const uint64_t z = (y | ((y << 1) & ~C0) | ((y >> 1) & ~C6) | (y >> 7) | (y << 7)) & A;
+    const bool moving = z != y;
+    x = z;
+    if (!ballot(moving)) break;
+  }
+  if (ballot(x != 0ull && (x & src) == src)) return 1;
+  return ballot(x != 0ull && (x & BORDER) == 0ull) ? 0 : -1;
+}
+
 // window cell c in [0,48) (v skipped) -> bit position and (di, dj) offsets from v
 __device__ __forceinline__ int window_pos(int c) { return c < 24 ? c : c + 1; }
 
@@ -593,7 +615,19 @@ struct Ctx {
       w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : (uint32_t)__popcll(bits & ~(1ull << lx));
       return;
     }
-    const int dx = GRID ? 4 : g.rowptr[x + 1] - g.rowptr[x];
+    if constexpr (GRID) {
+      // branch-free: the four reads issued together at clamped positions, then masked
+      const bool hu = xr > 0, hl = xc > 0, hr = xc < g.gw - 1, hd = xr < g.gh - 1;
+      const uint32_t lu = L(hu ? x - g.gw : x), ll = L(hl ? x - 1 : x);
+      const uint32_t lr = L(hr ? x + 1 : x), ld = L(hd ? x + g.gw : x);
+      bits = (hu ? 1ull << lu : 0ull) | (hl ? 1ull << ll : 0ull) | (hr ? 1ull << lr : 0ull) |
+             (hd ? 1ull << ld : 0ull);
+      cd = (uint32_t)(hu & (lu != lx)) + (uint32_t)(hl & (ll != lx)) + (uint32_t)(hr & (lr != lx)) +
+           (uint32_t)(hd & (ld != lx));
+      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : (uint32_t)__popcll(bits & ~(1ull << lx));
+      return;
+    }
+    const int dx = g.rowptr[x + 1] - g.rowptr[x];
     for (int j = 0; j < dx; ++j) {
       const int y = nbr(x, j, xr, xc);
       if (y < 0) continue;
@@ -648,24 +682,27 @@ struct Ctx {
       dv = degree(v, vr, vc);
       const int xr = vr + my_dr, xc = vc + my_dc;
       const bool ok = lane <= 8 && xr >= 0 && xr < g.gh && xc >= 0 && xc < g.gw;
+      // branch-free: every lane reads its cell and the cell's four neighbours at clamped
+      // positions (one LDS round trip), and the roles mask the results
+      const int xx = ok ? xr * g.gw + xc : v;
+      const uint32_t lxx = L(xx);
+      const bool hu = ok & (xr > 0), hl = ok & (xc > 0), hr = ok & (xc < g.gw - 1),
+                 hd = ok & (xr < g.gh - 1);
+      const uint32_t lu = L(hu ? xx - g.gw : xx), ll = L(hl ? xx - 1 : xx);
+      const uint32_t lr = L(hr ? xx + 1 : xx), ld = L(hd ? xx + g.gw : xx);
       if (!ok) return h;
-      h.x = xr * g.gw + xc;
-      h.lx = L(h.x);
+      h.x = xx;
+      h.lx = lxx;
       if (lane <= 4) {
-        h.deg = degree(h.x, xr, xc);
-        const int vslot = 4 - lane;  // up's down, left's right, right's left, down's up
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int y = nbr(h.x, j, xr, xc);
-          if (y < 0) continue;
-          if (lane > 0 && j == vslot) {
-            h.has_v = true;
-            continue;
-          }
-          const uint32_t ly = L(y);
-          h.bits |= 1ull << ly;
-          h.cnt += ly != h.lx;
-        }
+        h.deg = (int)hu + (int)hl + (int)hr + (int)hd;
+        // v's slot among the neighbour's neighbours: up's down, left's right, ...
+        const bool vu = lane == 4, vl = lane == 3, vrr = lane == 2, vd = lane == 1;
+        h.has_v = lane > 0;
+        const bool uu = hu & !vu, ul = hl & !vl, ur = hr & !vrr, ud = hd & !vd;
+        h.bits = (uu ? 1ull << lu : 0ull) | (ul ? 1ull << ll : 0ull) | (ur ? 1ull << lr : 0ull) |
+                 (ud ? 1ull << ld : 0ull);
+        h.cnt = (uint32_t)(uu & (lu != lxx)) + (uint32_t)(ul & (ll != lxx)) +
+                (uint32_t)(ur & (lr != lxx)) + (uint32_t)(ud & (ld != lxx));
       }
     } else if constexpr (E16) {
       // lanes 1..16 read v's padded row: its neighbours (a prefix) and so its degree
@@ -944,7 +981,7 @@ struct Ctx {
                         L(rr * g.gw + cc) == a;
         const uint64_t b48 = ballot(in) & ((1ull << 48) - 1ull);
         const uint64_t A = (b48 & ((1ull << 24) - 1ull)) | ((b48 >> 24) << 25);
-        const int wv = window_verdict(A);
+        const int wv = window_verdict_lanes(A, lane);
 #ifdef FW_STAMPS
         n_win += 1;
 #endif
