@@ -148,6 +148,8 @@ struct fw_chains {
   uint32_t* d_spill = nullptr;
   int32_t* d_next = nullptr;
   uint64_t max_yields = 0;  // upper bound on any chain's yield count (maps need < 2^32)
+  bool gcache_ok = false;   // the label records' group sums and the stats' cut / bnodes /
+                            // npairs match the labels (FwRunParams::gcache_ok)
   bool ran = false;
   // spatial observables (fw_chains_enable_maps)
   int64_t* d_acc = nullptr;
@@ -528,7 +530,9 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
                   init_per_chain ? (" " + std::to_string(i)).c_str() : "", why.c_str());
     }
   }
-  const int lab_stride = p.lab_bytes;
+  // a chain's HBM record also holds its group sums (derived-state cache, FwRunParams)
+  const int lab_stride = p.lab_bytes + (int)round16((int64_t)4 * (use16 ? (G + 1) / 2
+                                                                       : fw_run_gsum_words(G)));
   std::vector<uint8_t> packed((size_t)n_chains * lab_stride);
   std::vector<int64_t> pops((size_t)n_chains * k);
   {
@@ -558,6 +562,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.seed = seed;
   p.chain_id0 = chain_id0;
   p.lab_stride = lab_stride;
+  p.lab_copy16 = lab_stride / 16;
+  p.gcache_ok = 0;
   p.thr_stride = thr_per_chain ? 2 * D + 1 : 0;
   p.lb = lb;
   p.use16 = use16 ? 1 : 0;
@@ -565,6 +571,11 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
              : fw_run_grid_size(p, lb, g->device, &c->grid)) != 0) {
     delete c;
     return fail(FW_EHIP, "occupancy query failed (LDS %d B)", use16 ? p.lds16 : p.lds_bytes);
+  }
+  {  // FLIPWALK_GRID_CAP=x: at most x workgroups (tests: more work units than waves)
+    const char* e = getenv("FLIPWALK_GRID_CAP");
+    const int v = e && e[0] ? atoi(e) : 0;
+    if (v >= 1 && v < c->grid) c->grid = v;
   }
   const size_t nthr = (size_t)(thr_per_chain ? n_chains : 1) * (2 * D + 1);
   std::vector<uint64_t> thr53(nthr);
@@ -638,9 +649,14 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
   for (int64_t left = steps; left > 0;) {
     const int64_t s = left < cap ? left : cap;
     c->p.steps = s;
+    c->p.gcache_ok = c->gcache_ok ? 1 : 0;
     HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
     const int le = fw_launch_run(c->p, c->lb, c->grid, c->stream);
-    if (le != 0) return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString((hipError_t)le));
+    if (le != 0) {
+      c->gcache_ok = false;
+      return fail(FW_EHIP, "kernel launch failed: %s", hipGetErrorString((hipError_t)le));
+    }
+    c->gcache_ok = true;  // this launch writes every chain's record back
     left -= s;
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -773,6 +789,7 @@ int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t byt
         pack_labels(lab + (size_t)i * n, n, c->lb, packed.data() + (size_t)i * c->p.lab_stride,
                     c->p.lab_stride);
       }
+      c->gcache_ok = false;  // group sums and counts are re-derived from the new plans
       HIPCHK(hipMemcpy(c->d_labels, packed.data(), packed.size(), hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(c->d_pops, pops.data(), sizeof(int64_t) * pops.size(),
                        hipMemcpyHostToDevice));
@@ -781,6 +798,7 @@ int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t byt
     case FW_READ_STATS:
       need = sizeof(fw_chain_stats) * c->n_chains;
       if (bytes < need) return fail(FW_EINVAL, "stats need %zu bytes", need);
+      c->gcache_ok = false;  // cut / bnodes / npairs come from the caller's records
       HIPCHK(hipMemcpy(c->d_stats, host_src, need, hipMemcpyHostToDevice));
       c->ran = true;  // the initial state was yielded in the run being resumed
       return FW_OK;

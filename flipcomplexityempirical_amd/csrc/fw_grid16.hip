@@ -630,12 +630,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     const bool has = c < p.n_chains;
     const int cc = has ? c : cbase;  // a valid index for loads of absent rows
     const uint64_t gid = (uint64_t)(p.chain_id0 + c);
+    const bool cached = p.gcache_ok != 0;  // derived-state cache (FwRunParams)
 
     // ---- load state (each row loads its own chain)
     {
       const u32x4* src = reinterpret_cast<const u32x4*>(p.labels + (size_t)cc * p.lab_stride);
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(lab);
-      for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
+      // with a valid derived-state cache the slot's group sums come along (see lab_copy16)
+      const int nv = cached ? p.lab_copy16 : p.lab_bytes / 16;
+      for (int i = q; i < nv; i += ROW) dst[i] = src[i];
     }
     int32_t pops = q < k ? (int32_t)p.pops[(size_t)cc * k + q] : 0;  // total pop < 2^31
     double thr_l = FULL && q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
@@ -673,11 +676,12 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     int32_t bcnt = rule == FW_ACCEPT_BOUNDARY && q < k ? p.bcnt[(size_t)cc * k + q] : 0;
     lds_order();
 
-    // ---- derive group sums, cut / boundary / proposal-set counts (per row)
+    // ---- derive group sums, cut / boundary / proposal-set counts (per row), unless the
+    // derived-state cache holds them (group sums loaded with the labels, counts in stats)
     int32_t cut, bnodes, npairs;
     {
       uint32_t cut2 = 0, bn = 0, np = 0;
-      for (int t2 = 0; t2 < GW; ++t2) {
+      for (int t2 = 0; t2 < (cached ? 0 : GW); ++t2) {
         uint32_t tot[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -716,9 +720,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         for (int t2 = GW + q; t2 < 8 * PER; t2 += ROW)
           if (has) gsum[t2] = 0u;
       }
-      cut = (int32_t)(row_sum(cut2) / 2);
-      bnodes = (int32_t)row_sum(bn);
-      npairs = (int32_t)row_sum(np);
+      if (cached) {
+        cut = stp->cut;
+        bnodes = stp->bnodes;
+        npairs = stp->npairs;
+      } else {
+        cut = (int32_t)(row_sum(cut2) / 2);
+        bnodes = (int32_t)row_sum(bn);
+        npairs = (int32_t)row_sum(np);
+      }
     }
     lds_order();
     double invb = p.g.invb[bnodes];  // 1/|B| from the graph's table, no fp64 divide
@@ -1243,7 +1253,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (FULL && RN && q == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
-      for (int i = q; i < p.lab_bytes / 16; i += ROW) dst[i] = src[i];
+      for (int i = q; i < p.lab_copy16; i += ROW) dst[i] = src[i];  // labels + group sums
       if (q < k) p.pops[(size_t)c * k + q] = (int64_t)pops;
       if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
       if (q == 0 && maps_on) pend_store(p, c, pend);

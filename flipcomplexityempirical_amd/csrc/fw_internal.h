@@ -74,6 +74,14 @@ struct FwRunParams {
   int32_t no_rowbb;            // 1: large grids skip the row-parallel bitboard form (A/B)
   int32_t wpe5;                // 1: the 5-waves-per-SIMD chain-kernel instantiation
   int32_t lds16;               // dynamic LDS bytes per workgroup
+  // derived-state cache.  A chain's HBM label record (lab_stride bytes) mirrors the start
+  // of its LDS slot: labels, then the group sums (grid kernel: u16 pairs; chain kernel:
+  // the padded u32 layout of gsum_slot).  Each launch writes the first
+  // lab_copy16 16-B pieces back; when gcache_ok the next launch loads them all and takes
+  // cut / bnodes / npairs from the stats record instead of re-deriving them from every
+  // node's neighbourhood (host writes of labels or stats clear gcache_ok)
+  int32_t lab_copy16;
+  int32_t gcache_ok;
   // spatial observables (nullptr: off).  Per chain c: acc [E] (int64: sum of -t when an
   // edge becomes cut and +t when it becomes uncut, so cut_times = acc + [cut now] * Y),
   // nf / lf [n] (num_flips, last_flipped of finished runs), ps [n] (part_sum), and the

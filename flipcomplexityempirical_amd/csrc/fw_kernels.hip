@@ -89,11 +89,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (c >= p.n_chains) break;
     const uint64_t gid = (uint64_t)(p.chain_id0 + c);
 
-    // ---- load state
+    // ---- load state (with a valid derived-state cache the group sums that follow the
+    // labels in the chain's record come along: FwRunParams::lab_copy16)
+    const bool cached = p.gcache_ok != 0;
     {
       const u32x4* src = reinterpret_cast<const u32x4*>(p.labels + (size_t)c * p.lab_stride);
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(C.lab);
-      for (int i = lane; i < p.lab_bytes / 16; i += WAVE) dst[i] = src[i];
+      const int nv = cached ? p.lab_copy16 : p.lab_bytes / 16;
+      for (int i = lane; i < nv; i += WAVE) dst[i] = src[i];
     }
     int64_t pops = lane < k ? p.pops[(size_t)c * k + lane] : 0;  // lane d holds district d
     double thr_l = lane < 2 * D + 1 ? p.thr[(size_t)c * p.thr_stride + lane] : 0.0;
@@ -122,9 +125,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     int32_t bcnt = p.accept == FW_ACCEPT_BOUNDARY && lane < k ? p.bcnt[(size_t)c * k + lane] : 0;
     __syncthreads();
 
-    // ---- derive group sums, cut count, boundary count, proposal-set size
+    // ---- derive group sums, cut count, boundary count, proposal-set size (unless cached)
     int32_t cut, bnodes, npairs;
-    {
+    if (cached) {
+      cut = rfl(stp->cut);
+      bnodes = rfl(stp->bnodes);
+      npairs = rfl(stp->npairs);
+    } else {
       uint32_t cut2 = 0, bn = 0, np = 0;
       for (int t = 0; t < G; ++t) {
         const int x = t * 64 + lane;
@@ -371,7 +378,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     {
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(C.lab);
-      for (int i = lane; i < p.lab_bytes / 16; i += WAVE) dst[i] = src[i];
+      for (int i = lane; i < p.lab_copy16; i += WAVE) dst[i] = src[i];  // labels + group sums
       if (lane < k) p.pops[(size_t)c * k + lane] = pops;
       if (lane < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lane] = bcnt;
     }

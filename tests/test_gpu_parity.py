@@ -385,6 +385,22 @@ def test_long_run_split_into_launches(gpu_lib, name, path, monkeypatch):
     _run_vs_oracle(case, 11, [1000, 333])
 
 
+@pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("sec11_a2_k2", "auto"),
+                                       ("grid16x24_k8", "auto"), ("grid20_k4_mu", "wave64")])
+def test_many_units_per_wave(gpu_lib, name, path, monkeypatch):
+    """FLIPWALK_GRID_CAP=1 leaves one workgroup, so every wave runs many chains (quads)
+    one after another through the work counter, and the grid kernel's later launches load
+    each chain's group sums from its record (the derived-state cache) instead of deriving
+    them; trajectories and totals equal one oracle run."""
+    monkeypatch.setenv("FLIPWALK_GRID_CAP", "1")
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    _run_vs_oracle(case, 37, [600, 250, 150])
+
+
 @pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
                                        ("sec11_a2_k2", "auto"), ("tract_k4", "auto")])
 def test_checkpoint_resume_bit_exact(gpu_lib, name, path, monkeypatch, tmp_path):
