@@ -147,6 +147,7 @@ struct fw_chains {
   unsigned long long* d_hist_b = nullptr;
   uint32_t* d_spill = nullptr;
   int32_t* d_next = nullptr;
+  uint32_t* d_gscr = nullptr;  // chain kernel, 3-bit labels: search marks
   uint64_t max_yields = 0;  // upper bound on any chain's yield count (maps need < 2^32)
   bool gcache_ok = false;   // the label records' group sums and the stats' cut / bnodes /
                             // npairs match the labels (FwRunParams::gcache_ok)
@@ -446,7 +447,7 @@ void fw_chains_destroy(fw_chains* c) {
   void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_thr53, c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
                   c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt, c->d_sched, c->d_sched53,
-                  c->d_ring,   c->d_ring_node, c->d_hist_ring};
+                  c->d_ring,   c->d_ring_node, c->d_hist_ring, c->d_gscr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -478,7 +479,14 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   for (int x = 0; x < n; ++x) total_pop += g->popof(x);
   const bool use16 = fw_grid16_candidate(g->gw, D, G, k, total_pop) && g->gm24 != 0 &&
                      !(no16 && no16[0] == '1');
-  const int lb = use16 ? fw_grid16_lb(G, k) : pick_lb(k, g->maxdeg);
+  int lb = use16 ? fw_grid16_lb(G, k) : pick_lb(k, g->maxdeg);
+  {  // the chain kernel on a large grid (k <= 8): 3-bit labels in LDS, search marks in HBM,
+     // so more chains fit a CU (C5: 7 -> 9).  FLIPWALK_CSR_LB=3 / 4 forces / forbids it.
+    const char* e = getenv("FLIPWALK_CSR_LB");
+    const int want = e && e[0] ? atoi(e) : 0;
+    if (!use16 && g->gw > 0 && k <= 8 && lb == 4 && (want == 3 || (want == 0 && G > 256)))
+      lb = 3;
+  }
   if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 
   auto c = new fw_chains();
@@ -621,6 +629,15 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.hist_b = c->d_hist_b;
   p.spill = c->d_spill;
   p.next_chain = c->d_next;
+  if (lb == 3 && !use16) {  // HBM visit marks of the chain kernel's list search (all zero)
+    p.gscr_words = (n + 7) / 8;
+    const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
+    if (hipMalloc(&c->d_gscr, gb) != hipSuccess || hipMemset(c->d_gscr, 0, gb) != hipSuccess) {
+      fw_chains_destroy(c);
+      return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
+    }
+    p.gscr = c->d_gscr;
+  }
   *out = c;
   return FW_OK;
 }

@@ -530,6 +530,8 @@ struct Ctx {
   LDS uint32_t* gsum;
   LDS uint32_t* list;  // LDS part of the search list
   GLB uint32_t* spill; // HBM part (this workgroup's slice)
+  GLB uint32_t* gscr;  // LB == 3: this workgroup's 4-bit visit marks in HBM (all zero
+                       // between searches; 3-bit labels cannot hold the search codes)
   int32_t qcap, k;
   int lane;
   bool bb;  // grids: exact searches try the bitboard form first
@@ -805,6 +807,125 @@ struct Ctx {
   }
 
   // -------------------------------------------------------------- contiguity
+  // -- 4-bit visit marks in HBM (LB == 3).  Agent-scope atomics and loads: the marks are
+  // read back within the same search, so no access may be served by a stale L1 line.
+  __device__ __forceinline__ uint32_t gs_get(int x) const {
+    return (__hip_atomic_load(gscr + (x >> 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
+            ((x & 7) << 2)) & 15u;
+  }
+  __device__ __forceinline__ void gs_xor(int x, uint32_t d) const {
+    __hip_atomic_fetch_xor(gscr + (x >> 3), d << ((x & 7) << 2), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ void gs_clear(int x) const {
+    __hip_atomic_fetch_and(gscr + (x >> 3), ~(15u << ((x & 7) << 2)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // claim mark x: 0 -> code if still unvisited; returns the mark found (0 on success)
+  __device__ __forceinline__ uint32_t gs_claim(int x, uint32_t code) const {
+    GLB uint32_t* w = gscr + (x >> 3);
+    const int sh = (x & 7) << 2;
+    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const uint32_t cur = (old >> sh) & 15u;
+      if (cur != 0u) return cur;
+      if (__hip_atomic_compare_exchange_strong(w, &old, old | (code << sh), __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        return 0u;
+    }
+  }
+
+  // The race search with the visit marks in gscr (1 + source index, 15 = v) instead of in
+  // the labels: the same levels, pushes, merges and counters as race_search (and as the
+  // grid kernel's grid_race); grids only.
+  __device__ bool race_search_gscr(int v, uint32_t a, int m, int src, uint64_t cls,
+                                   uint64_t& bfs_nodes, uint64_t& bfs_deg) {
+    if (lane == 0) gs_xor(v, 15u);
+    if (lane < m) {
+      gs_xor(src, 1u + (uint32_t)lane);
+      list_put(lane, (uint32_t)src);
+    }
+    __threadfence_block();
+    int nl = m, lb = 0, le = m;
+    uint32_t my_deg = 0;
+    int verdict = -1;
+    for (;;) {
+      uint64_t rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
+      if (__popcll(rep) == 1) {
+        verdict = 1;
+        break;
+      }
+      uint64_t pushed_src = 0;
+      for (int base = lb; base < le; base += WAVE) {
+        const int idx = base + lane;
+        const bool act = idx < le;
+        const int x = act ? (int)list_get(idx) : 0;
+        const uint32_t o = act ? gs_get(x) - 1u : 0u;
+        int xr = 0, xc = 0;
+        if (act) {
+          divmod(x, xr, xc);
+          my_deg += (uint32_t)degree(x, xr, xc);
+        }
+        bfs_nodes += (uint64_t)__popcll(ballot(act));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int y = act ? nbr(x, j, xr, xc) : -1;
+          bool push = false, req = false;
+          uint32_t other = 0;
+          if (y >= 0 && L(y) == a) {
+            const uint32_t got = gs_claim(y, 1u + o);
+            if (got == 0u) {
+              push = true;
+            } else if (got - 1u < (uint32_t)m) {  // v (15) is never a class
+              req = true;
+              other = got - 1u;
+            }
+          }
+          const uint64_t pm = ballot(push);
+          if (push) list_put(nl + (int)mbcnt(pm), (uint32_t)y);
+          nl += __popcll(pm);
+          if (pm) {
+            for (int si = 0; si < m; ++si)
+              pushed_src |= ballot(push && o == (uint32_t)si) ? (1ull << si) : 0ull;
+          }
+          uint64_t rm = ballot(req && o != other);
+          while (rm) {  // merges, serial over requesting lanes
+            const int Lr = __ffsll((unsigned long long)rm) - 1;
+            rm &= rm - 1;
+            const int o1 = rdl((int32_t)o, Lr), o2 = rdl((int32_t)other, Lr);
+            const uint64_t m1 = rdl64(cls, o1), m2 = rdl64(cls, o2);
+            if (m1 != m2) {
+              const uint64_t nm = m1 | m2;
+              if (lane < m && ((nm >> lane) & 1ull)) cls = nm;
+            }
+          }
+        }
+        __threadfence_block();  // marks and spilled entries are read next level
+      }
+      lds_order();
+      lb = le;
+      le = nl;
+      rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
+      if (__popcll(rep) == 1) {
+        verdict = 1;
+        break;
+      }
+      const bool closed = lane < m && ((rep >> lane) & 1ull) && ((cls & pushed_src) == 0ull);
+      if (ballot(closed)) {
+        verdict = 0;
+        break;
+      }
+    }
+    bfs_deg += wave_sum(my_deg);
+    for (int base = 0; base < nl; base += WAVE) {  // clear the visit marks
+      const int idx = base + lane;
+      if (idx < nl) gs_clear((int)list_get(idx));
+    }
+    if (lane == 0) gs_clear(v);
+    __threadfence_block();
+    return verdict == 1;
+  }
+
   // Exact verdict on "(district a) minus v is connected and non-empty", by a
   // level-synchronous race search from the m a-labelled neighbours of v (the
   // sources, in CSR order); cls holds, in lanes 0..m-1, the pre-merged class masks.
@@ -1021,7 +1142,10 @@ struct Ctx {
       const int val = rdl(h.x, Ls);
       if (lane == i) src = val;
     }
-    return race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);
+    if constexpr (LB == 3)
+      return race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
+    else
+      return race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);
   }
 };
 

@@ -68,6 +68,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   C.gsum = reinterpret_cast<LDS uint32_t*>(sm + p.off_gsum);
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
+  C.gscr = LB == 3 ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
   C.qcap = p.qcap;
   C.k = p.k;
   C.bb = true;
@@ -574,6 +575,9 @@ void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false) 
     if (e16) return cut ? pick_per<4, false, 2, true>(G) : pick_per<4, false, 1, true>(G);
     return cut ? pick_per<4, false, 2, false>(G) : pick_per<4, false, 1, false>(G);
   }
+  if (lb == 3)  // grids, k <= 8 (the large-grid LDS plan: fw_chains_create)
+    return grid ? (cut ? pick_per<3, true, 2, false, 3>(G) : pick_per<3, true, 1, false, 3>(G))
+                : nullptr;  // <= 3 waves per SIMD: LDS holds 9 chains per CU
   if (grid) return cut ? pick_per<8, true, 2, false>(G) : pick_per<8, true, 1, false>(G);
   if (e16) return cut ? pick_per<8, false, 2, true>(G) : pick_per<8, false, 1, true>(G);
   return cut ? pick_per<8, false, 2, false>(G) : pick_per<8, false, 1, false>(G);
@@ -594,11 +598,14 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   // down to 128 entries (longer searches continue in the HBM spill area), when that keeps
   // one more chain per CU; the longest list that reaches the best residency is kept.
   // FLIPWALK_LIST_CAP pins the length (tests of the spill path).
+  // With 3-bit labels the list search (a rare fallback past the bitboard window) keeps its
+  // marks in HBM anyway, and the list may shrink to 16 entries.
   const char* cap_env = getenv("FLIPWALK_LIST_CAP");
-  if (!(cap_env && cap_env[0]) && p.qcap > 128) {
+  const int q_min = lb == 3 ? 16 : 128;
+  if (!(cap_env && cap_env[0]) && p.qcap > q_min) {
     const int base = p.off_list;
     int best_q = p.qcap, best = per_cu;
-    for (int q = p.qcap - 8; q >= 128; q -= 8) {
+    for (int q = p.qcap - 8; q >= q_min; q -= 8) {
       const int lds = base + 4 * q;
       if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -1;

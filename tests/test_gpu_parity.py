@@ -222,14 +222,22 @@ def test_accept_rules_bit_exact(gpu_lib, name, rule, path, monkeypatch):
             assert st[f][i] == ost[f][0], (name, i, f)
 
 
-@pytest.mark.parametrize("n,k,bw", [(132, 8, 4), (200, 8, 4)])
-def test_large_grid_ladder_bit_exact(gpu_lib, n, k, bw, monkeypatch):
+@pytest.mark.parametrize("n,k,bw,variant", [(132, 8, 4, "auto"), (200, 8, 4, "auto"),
+                                            (200, 8, 4, "lb4"), (200, 8, 4, "list")])
+def test_large_grid_ladder_bit_exact(gpu_lib, n, k, bw, variant, monkeypatch):
     """C5 shape: grids past the four-chains-per-wave kernel's 16,384-node limit (one chain
     per wave, implicit grid neighbours, 16 group sums per lane) with per-chain Metropolis
-    bases from the C5 ladder (thr_per_chain)."""
+    bases from the C5 ladder (thr_per_chain).  auto: 3-bit labels with the list search's
+    marks in HBM; lb4: 4-bit labels with in-place marks; list: 3-bit labels, every exact
+    search as the HBM-marked list search with a 2-entry LDS list (spill)."""
     from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
     from flipcomplexityempirical_amd.graph import block_seed, grid_graph
     monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    if variant == "lb4":
+        monkeypatch.setenv("FLIPWALK_CSR_LB", "4")
+    if variant == "list":
+        monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
+        monkeypatch.setenv("FLIPWALK_LIST_CAP", "2")
     g = grid_graph(n, n)
     init = block_seed(n, n, 2, bw)
     bounds = population_bounds(g.total_pop, k, 0.05)
@@ -383,6 +391,23 @@ def test_long_run_split_into_launches(gpu_lib, name, path, monkeypatch):
     monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
     case = {c.name: c for c in CASES}[name]
     _run_vs_oracle(case, 11, [1000, 333])
+
+
+@pytest.mark.parametrize("name", ["grid20_k4_mu", "grid16x24_k8", "grid30x18_k2_bi"])
+@pytest.mark.parametrize("search", ["bitboard", "list"])
+def test_chain_kernel_3bit_labels(gpu_lib, name, search, monkeypatch):
+    """The one-chain-per-wave kernel with 3-bit labels (FLIPWALK_CSR_LB=3; the default on
+    large grids with k <= 8): labels straddle bytes, and the list search keeps its visit
+    marks in HBM instead of in the labels (list: forced for every exact search, with a
+    2-entry LDS list so the visit list spills too)."""
+    monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    monkeypatch.setenv("FLIPWALK_CSR_LB", "3")
+    if search == "list":
+        monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
+        monkeypatch.setenv("FLIPWALK_LIST_CAP", "2")
+    case = {c.name: c for c in CASES}[name]
+    st = _run_vs_oracle(case, 29, [400, 300])
+    assert st["bfs_runs"].sum() > 0
 
 
 @pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("sec11_a2_k2", "auto"),
