@@ -515,7 +515,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   // +8: the grid kernels read label dwords one past the last node
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
   p.off_gsum = p.lab_bytes;
-  p.off_list = p.off_gsum + round16((int64_t)fw_run_gsum_words(G) * 4);
+  p.off_list = p.off_gsum + round16((int64_t)fw_run_gsum_slots(G) * 2);  // u16 slots
   p.lds_bytes = p.off_list + p.qcap * 4;
   if (G > 64 * 16) {
     delete c;
@@ -540,7 +540,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   }
   // a chain's HBM record also holds its group sums (derived-state cache, FwRunParams)
   const int lab_stride = p.lab_bytes + (int)round16((int64_t)4 * (use16 ? (G + 1) / 2
-                                                                       : fw_run_gsum_words(G)));
+                                                                       : (fw_run_gsum_slots(G) + 1) / 2));
   std::vector<uint8_t> packed((size_t)n_chains * lab_stride);
   std::vector<int64_t> pops((size_t)n_chains * k);
   {

@@ -527,7 +527,7 @@ struct Ctx {
   using P = PK<LB>;
   FwGraphDev g;
   LDS uint8_t* lab;
-  LDS uint32_t* gsum;
+  LDS uint16_t* gsum;  // u16 group sums (<= 64 nodes x weight <= 63), gsum_slot layout
   LDS uint32_t* list;  // LDS part of the search list
   GLB uint32_t* spill; // HBM part (this workgroup's slice)
   GLB uint32_t* gscr;  // LB == 3: this workgroup's 4-bit visit marks in HBM (all zero

@@ -152,7 +152,7 @@ int fw_launch_bcnt_init(const FwRunParams& p, void* stream);
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream);
 int fw_launch_eval(const FwEvalParams& p, int lb, int grid, void* stream);
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid);
-int fw_run_gsum_words(int G);
+int fw_run_gsum_slots(int G);  // u16 group-sum slots of the chain kernel
 // fw_grid16.hip
 bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop);
 int fw_grid16_lb(int G, int k);

@@ -5,7 +5,7 @@
 // for the whole launch:
 //   lab   packed LB-bit district labels (LB = 4: 0.5 B/node; LB = 8: 1 B/node).  The
 //         contiguity search marks visited nodes in place with codes k..k+deg-1.
-//   gsum  u32 proposal-weight sum per 64-node group (rank/select level 1)
+//   gsum  u16 proposal-weight sum per 64-node group (rank/select level 1)
 //   list  the contiguity search's visit list (spills to HBM past qcap entries)
 // Per-node proposal weights (#distinct foreign labels, or cut degree) are recomputed
 // from labels where needed instead of being stored, which halves LDS per chain and
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   C.g = p.g;
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
   C.lab = sm;
-  C.gsum = reinterpret_cast<LDS uint32_t*>(sm + p.off_gsum);
+  C.gsum = reinterpret_cast<LDS uint16_t*>(sm + p.off_gsum);
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.gscr = LB == 3 ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         uint32_t w = 0, cd = 0;
         if (x < n) C.template weight_now<MODE>(x, w, cd);
         const uint32_t gsum_t = wave_sum(w);
-        if (lane == 0) C.gsum[gsum_slot<PER>(t)] = gsum_t;
+        if (lane == 0) C.gsum[gsum_slot<PER>(t)] = (uint16_t)gsum_t;  // <= 64 x 63
         cut2 += cd;
         bn += cd > 0;
         np += w;
@@ -345,7 +345,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (p.sched) sched_row(n_acc);
         n_adeg += (uint32_t)dv;
         if (lane == 0) PK<LB>::axor(C.lab, v, a ^ d);
-        if (mine && h.x >= 0 && wn != wo) lds_add(C.gsum + gsum_slot<PER>(h.x >> 6), wn - wo);
+        if (mine && h.x >= 0 && wn != wo) {
+          // u16 slot inside its u32 word: a wrapping 32-bit add of the shifted delta changes
+          // only that half (both halves stay in [0, 65535])
+          const int sl = gsum_slot<PER>(h.x >> 6);
+          lds_add(reinterpret_cast<LDS uint32_t*>(C.gsum) + (sl >> 1), (wn - wo) << (16 * (sl & 1)));
+        }
         lds_order();
         npairs += (int32_t)wave_sum(mine ? wn - wo : 0u);
         cut += dcut;
@@ -544,10 +549,10 @@ extern "C" int fw_debug_stamps_csr(unsigned long long* out, int reset) {
 }
 #endif
 
-// group sums per lane of the one-chain-per-wave kernel (pick_per) and the LDS words its
-// padded level-1 layout (gsum_slot) takes for G groups
+// group sums per lane of the one-chain-per-wave kernel (pick_per) and the u16 LDS slots
+// its padded level-1 layout (gsum_slot) takes for G groups
 int fw_run_per(int G) { return G <= 64 * 2 ? 2 : G <= 64 * 4 ? 4 : G <= 64 * 8 ? 8 : 16; }
-int fw_run_gsum_words(int G) {
+int fw_run_gsum_slots(int G) {
   const int per = fw_run_per(G);
   return G <= 0 ? 0 : ((G - 1) / per) * (per + 1) + (G - 1) % per + 1;
 }
@@ -599,9 +604,9 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   // one more chain per CU; the longest list that reaches the best residency is kept.
   // FLIPWALK_LIST_CAP pins the length (tests of the spill path).
   // With 3-bit labels the list search (a rare fallback past the bitboard window) keeps its
-  // marks in HBM anyway, and the list may shrink to 16 entries.
+  // marks in HBM anyway, and the list may shrink to 8 entries.
   const char* cap_env = getenv("FLIPWALK_LIST_CAP");
-  const int q_min = lb == 3 ? 16 : 128;
+  const int q_min = lb == 3 ? 8 : 128;
   if (!(cap_env && cap_env[0]) && p.qcap > q_min) {
     const int base = p.off_list;
     int best_q = p.qcap, best = per_cu;
