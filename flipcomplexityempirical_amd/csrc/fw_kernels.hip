@@ -249,6 +249,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           break;
         }
         j = rfl(j);
+        // v's population, read before the neighbourhood so the table read (C4: lognormal
+        // populations in HBM / L2) overlaps the LDS round trip instead of following it
+        pv = unit_pop ? 1 : p.g.pop[v];
         // ---- v's neighbourhood (one LDS round trip)
         h = C.gather(v, dv);
         dv = rfl(dv);
@@ -276,7 +279,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         nbd = __popcll(ballot(isnb && h.lx == d));
         dcut = m - nbd;
         // ---- population bound (Bounds over the two changed districts)
-        pv = unit_pop ? 1 : p.g.pop[v];
         const int64_t pa = (int64_t)rdl64((uint64_t)pops, (int)a);
         const int64_t pb = (int64_t)rdl64((uint64_t)pops, (int)d);
         if (pa - pv < p.pop_lo || pb + pv > p.pop_hi) {
@@ -356,7 +358,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         cut += dcut;
         bnodes += plus - minus;
         n_bchg += (uint32_t)(plus + minus);
-        if (plus | minus) invb = p.g.invb[bnodes];
+        // 1/|B| by the IEEE double division (= the host table and the oracle's 1.0/b):
+        // ~150 cycles of fp64 ops instead of an exposed L2 round trip to the table
+        if (plus | minus) invb = 1.0 / (double)max(bnodes, 1);
         if (lane == (int)a) pops -= pv;
         if (lane == (int)d) pops += pv;
         if (p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
