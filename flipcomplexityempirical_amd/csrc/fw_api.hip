@@ -486,6 +486,15 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     const int want = e && e[0] ? atoi(e) : 0;
     if (!use16 && g->gw > 0 && k <= 8 && lb == 4 && (want == 3 || (want == 0 && G > 256)))
       lb = 3;
+    // general graphs on padded rows whose k + maxdeg needs 8-bit in-place codes: 5-bit
+    // labels with the marks in HBM once the labels dominate LDS (n > 16,384: 8-bit labels
+    // would hold fewer than 10 chains per CU).  C4 (9,000 nodes, k = 18) keeps 8 bits: 5 bits
+    // there reach 20 chains per CU only with the 5-wave register budget, which spills
+    // (0.495 vs 0.523 x 10^9, profiles/r02/ab/csr_5bit_c4.jsonl).  FLIPWALK_CSR_LB=5 / 8
+    // forces / forbids (5 also for k <= 15).
+    if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 &&
+        (want == 5 || (want == 0 && lb == 8 && n > 16384)))
+      lb = 5;
   }
   if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 
@@ -629,7 +638,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.hist_b = c->d_hist_b;
   p.spill = c->d_spill;
   p.next_chain = c->d_next;
-  if (lb == 3 && !use16) {  // HBM visit marks of the chain kernel's list search (all zero)
+  if ((lb == 3 || lb == 5) && !use16) {  // HBM visit marks of the chain kernel's list search
     p.gscr_words = (n + 7) / 8;
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
     if (hipMalloc(&c->d_gscr, gb) != hipSuccess || hipMemset(c->d_gscr, 0, gb) != hipSuccess) {

@@ -180,6 +180,25 @@ struct PK<3> {
   }
 };
 
+// 5-bit labels (the chain kernel on general graphs with 16 <= k <= 31, e.g. C4's k = 18;
+// the list search keeps its marks in HBM): the same dword-pair reads and straddle updates.
+template <>
+struct PK<5> {
+  static constexpr uint32_t MASK = 31u;
+  __device__ static __forceinline__ uint32_t get(const LDS uint8_t* b, int x) {
+    const LDS uint32_t* w = reinterpret_cast<const LDS uint32_t*>(b);
+    const int bit = 5 * x, wi = bit >> 5;
+    const uint64_t both = ((uint64_t)w[wi + 1] << 32) | w[wi];
+    return (uint32_t)(both >> (bit & 31)) & 31u;
+  }
+  __device__ static __forceinline__ void axor(LDS uint8_t* b, int x, uint32_t d) {
+    LDS uint32_t* w = reinterpret_cast<LDS uint32_t*>(b);
+    const int bit = 5 * x, wi = bit >> 5, sh = bit & 31;
+    __atomic_fetch_xor(w + wi, d << sh, __ATOMIC_RELAXED);
+    if (sh > 27) __atomic_fetch_xor(w + wi + 1, d >> (32 - sh), __ATOMIC_RELAXED);
+  }
+};
+
 __device__ __forceinline__ void lds_add(LDS uint32_t* p, uint32_t v) {
   __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
@@ -530,8 +549,8 @@ struct Ctx {
   LDS uint16_t* gsum;  // u16 group sums (<= 64 nodes x weight <= 63), gsum_slot layout
   LDS uint32_t* list;  // LDS part of the search list
   GLB uint32_t* spill; // HBM part (this workgroup's slice)
-  GLB uint32_t* gscr;  // LB == 3: this workgroup's 4-bit visit marks in HBM (all zero
-                       // between searches; 3-bit labels cannot hold the search codes)
+  GLB uint32_t* gscr;  // LB == 3, 5: this workgroup's 4-bit visit marks in HBM (all zero
+                       // between searches; such labels cannot hold the search codes)
   int32_t qcap, k;
   int lane;
   bool bb;  // grids: exact searches try the bitboard form first
@@ -836,8 +855,8 @@ struct Ctx {
   }
 
   // The race search with the visit marks in gscr (1 + source index, 15 = v) instead of in
-  // the labels: the same levels, pushes, merges and counters as race_search (and as the
-  // grid kernel's grid_race); grids only.
+  // the labels (3- and 5-bit labels cannot hold the codes): the same levels, pushes, merges
+  // and counters as race_search (and as the grid kernel's grid_race).
   __device__ bool race_search_gscr(int v, uint32_t a, int m, int src, uint64_t cls,
                                    uint64_t& bfs_nodes, uint64_t& bfs_deg) {
     if (lane == 0) gs_xor(v, 15u);
@@ -862,14 +881,35 @@ struct Ctx {
         const int x = act ? (int)list_get(idx) : 0;
         const uint32_t o = act ? gs_get(x) - 1u : 0u;
         int xr = 0, xc = 0;
-        if (act) {
-          divmod(x, xr, xc);
+        int dmax = 0;
+        int r16[16];
+        if constexpr (E16) {
+          if (act) {
+            row16(x, r16);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dmax += r16[j] >= 0 ? 1 : 0;
+            my_deg += (uint32_t)dmax;
+          }
+        } else if (act) {
+          if constexpr (GRID) divmod(x, xr, xc);
+          dmax = GRID ? 4 : g.rowptr[x + 1] - g.rowptr[x];
           my_deg += (uint32_t)degree(x, xr, xc);
         }
         bfs_nodes += (uint64_t)__popcll(ballot(act));
+        int jmax = 4;
+        if constexpr (!GRID) {
+          uint32_t dm = (uint32_t)dmax;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int y = act ? nbr(x, j, xr, xc) : -1;
+          for (int dd = 32; dd >= 1; dd >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, dd, WAVE));
+          jmax = (int)rfl(dm);
+        }
+        for (int j = 0; j < (E16 ? 16 : 64); ++j) {  // r16[j]: uniform j
+          if (j >= jmax) break;  // uniform
+          int y;
+          if constexpr (E16)
+            y = (act && j < dmax) ? r16[j] : -1;
+          else
+            y = (act && j < dmax) ? nbr(x, j, xr, xc) : -1;
           bool push = false, req = false;
           uint32_t other = 0;
           if (y >= 0 && L(y) == a) {
@@ -1142,7 +1182,7 @@ struct Ctx {
       const int val = rdl(h.x, Ls);
       if (lane == i) src = val;
     }
-    if constexpr (LB == 3)
+    if constexpr (LB == 3 || LB == 5)
       return race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else
       return race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   C.gsum = reinterpret_cast<LDS uint16_t*>(sm + p.off_gsum);
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
-  C.gscr = LB == 3 ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
+  C.gscr = LB == 3 || LB == 5 ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
   C.qcap = p.qcap;
   C.k = p.k;
   C.bb = true;
@@ -584,6 +584,10 @@ void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false) 
     if (e16) return cut ? pick_per<4, false, 2, true>(G) : pick_per<4, false, 1, true>(G);
     return cut ? pick_per<4, false, 2, false>(G) : pick_per<4, false, 1, false>(G);
   }
+  if (lb == 5)  // general graphs with padded rows, 16 <= k <= 31 (fw_chains_create)
+    return !grid && e16 ? (wpe5 ? (cut ? pick_per<5, false, 2, true, 5>(G) : pick_per<5, false, 1, true, 5>(G))
+                                : (cut ? pick_per<5, false, 2, true>(G) : pick_per<5, false, 1, true>(G)))
+                        : nullptr;
   if (lb == 3)  // grids, k <= 8 (the large-grid LDS plan: fw_chains_create)
     return grid ? (cut ? pick_per<3, true, 2, false, 3>(G) : pick_per<3, true, 1, false, 3>(G))
                 : nullptr;  // <= 3 waves per SIMD: LDS holds 9 chains per CU
@@ -610,7 +614,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   // With 3-bit labels the list search (a rare fallback past the bitboard window) keeps its
   // marks in HBM anyway, and the list may shrink to 8 entries.
   const char* cap_env = getenv("FLIPWALK_LIST_CAP");
-  const int q_min = lb == 3 ? 8 : 128;
+  const int q_min = lb == 3 || lb == 5 ? 8 : 128;
   if (!(cap_env && cap_env[0]) && p.qcap > q_min) {
     const int base = p.off_list;
     int best_q = p.qcap, best = per_cu;
@@ -636,7 +640,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   // 4-bit labels on padded rows: when LDS admits more chains per CU than the 4-wave
   // register budget, the 5-wave instantiation (Frankengraph: 16 -> 20 chains per CU, +4%)
   p.wpe5 = 0;
-  if (lb == 4 && p.g.gw == 0 && p.g.ell != nullptr) {
+  if ((lb == 4 || lb == 5) && p.g.gw == 0 && p.g.ell != nullptr) {
     void* fn5 = pick_run(lb, false, true, p.mode, p.G, true);
     if (hipFuncSetAttribute(fn5, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
         hipSuccess)

@@ -393,6 +393,24 @@ def test_long_run_split_into_launches(gpu_lib, name, path, monkeypatch):
     _run_vs_oracle(case, 11, [1000, 333])
 
 
+@pytest.mark.parametrize("name,lb,cap", [("delaunay3k_k18", "5", None), ("delaunay3k_k18", "5", "2"),
+                                         ("delaunay3k_k18", "8", None), ("tract_k4", "5", None),
+                                         ("frank_a2_k2", "5", "2")])
+def test_chain_kernel_5bit_labels(gpu_lib, name, lb, cap, monkeypatch):
+    """General graphs on padded rows: 5-bit labels (the default when k + maxdeg needs more
+    than 4 bits, C4's k = 18) with the list search's visit marks in HBM; FLIPWALK_CSR_LB=5
+    forces them for small k, =8 keeps the in-place 8-bit marks; cap=2 spills the list."""
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    monkeypatch.setenv("FLIPWALK_CSR_LB", lb)
+    if cap:
+        monkeypatch.setenv("FLIPWALK_LIST_CAP", cap)
+    case = {c.name: c for c in CASES}.get(name)
+    if case is None:
+        pytest.skip(f"{name}: fixture data absent")
+    st = _run_vs_oracle(case, 23, [300, 200])
+    assert st["bfs_runs"].sum() > 0
+
+
 @pytest.mark.parametrize("name", ["grid20_k4_mu", "grid16x24_k8", "grid30x18_k2_bi"])
 @pytest.mark.parametrize("search", ["bitboard", "list"])
 def test_chain_kernel_3bit_labels(gpu_lib, name, search, monkeypatch):
