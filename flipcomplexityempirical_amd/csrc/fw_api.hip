@@ -148,6 +148,7 @@ struct fw_chains {
   uint32_t* d_spill = nullptr;
   int32_t* d_next = nullptr;
   uint32_t* d_gscr = nullptr;  // chain kernel, 3-bit labels: search marks
+  int32_t* d_segdone = nullptr;  // grid kernel: finished slices per quad
   uint64_t max_yields = 0;  // upper bound on any chain's yield count (maps need < 2^32)
   bool gcache_ok = false;   // the label records' group sums and the stats' cut / bnodes /
                             // npairs match the labels (FwRunParams::gcache_ok)
@@ -447,7 +448,7 @@ void fw_chains_destroy(fw_chains* c) {
   void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_thr53, c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
                   c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt, c->d_sched, c->d_sched53,
-                  c->d_ring,   c->d_ring_node, c->d_hist_ring, c->d_gscr};
+                  c->d_ring,   c->d_ring_node, c->d_hist_ring, c->d_gscr, c->d_segdone};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -638,6 +639,14 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.hist_b = c->d_hist_b;
   p.spill = c->d_spill;
   p.next_chain = c->d_next;
+  p.slices = 1;
+  if (use16) {
+    if (hipMalloc(&c->d_segdone, sizeof(int32_t) * (size_t)((n_chains + 3) / 4)) != hipSuccess) {
+      fw_chains_destroy(c);
+      return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
+    }
+    p.seg_done = c->d_segdone;
+  }
   if ((lb == 3 || lb == 5) && !use16) {  // HBM visit marks of the chain kernel's list search
     p.gscr_words = (n + 7) / 8;
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
@@ -649,6 +658,30 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   }
   *out = c;
   return FW_OK;
+}
+
+// Slices per quad for a grid-kernel launch of `steps` steps (see fw_grid16_kernel): with
+// more quads than resident waves W, the S in 1..4 that minimises a uniform-duration model
+// of the launch, ceil(nq S / W) / S rounds of whole-quad time plus ~0.6% of a quad's time
+// per extra slice start (measured: three 333-step launches cost 1.2% more than one
+// 1000-step launch net of their tails).  FLIPWALK_SLICES=x forces x (1: whole quads).
+static int grid16_slices(const fw_chains* c, int64_t steps) {
+  const char* e = getenv("FLIPWALK_SLICES");
+  const int force = e && e[0] ? atoi(e) : 0;
+  const long long nq = (c->n_chains + 3) / 4, W = (long long)c->grid * c->p.nw;
+  if (force >= 1) return (int)std::min<long long>(force, std::max<int64_t>(steps, 1));
+  if (nq <= W || steps < 64) return 1;
+  int best = 1;
+  double best_t = 1e300;
+  for (int S = 1; S <= 4; ++S) {
+    const double rounds = (double)((nq * S + W - 1) / W) / S;
+    const double t = rounds + 0.006 * (S - 1) * (double)nq / (double)W;
+    if (t < best_t - 1e-9) {
+      best_t = t;
+      best = S;
+    }
+  }
+  return best;
 }
 
 int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
@@ -676,6 +709,10 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
     const int64_t s = left < cap ? left : cap;
     c->p.steps = s;
     c->p.gcache_ok = c->gcache_ok ? 1 : 0;
+    c->p.slices = c->p.use16 && !c->p.trace ? grid16_slices(c, s) : 1;
+    if (c->p.slices > 1)
+      HIPCHK(hipMemsetAsync(c->d_segdone, 0, sizeof(int32_t) * (size_t)((c->n_chains + 3) / 4),
+                            c->stream));
     HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
     const int le = fw_launch_run(c->p, c->lb, c->grid, c->stream);
     if (le != 0) {

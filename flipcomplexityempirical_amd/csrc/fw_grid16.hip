@@ -621,16 +621,41 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   }
   __syncthreads();
 
+  // Work units: quad (four chains, one per row) x slice of the launch's steps, handed out
+  // slice-major (unit u = slice u / nq of quad u % nq; p.slices = 1: whole quads).  With
+  // more quads than resident waves the host picks the slice count that makes the units a
+  // whole number of residency rounds (65,536 chains: 16,384 quads x 3 = 16 rounds of 3,072
+  // waves), so the launch does not end on a partly filled round.  A slice starts once its
+  // quad's previous slice is written back (seg_done, agent-scope release / acquire: the
+  // previous slice ran a round or more earlier, so the wait is normally already over); the
+  // trajectory equals separate launches of the slices' step counts.
+  const int nq = (p.n_chains + 3) >> 2;
   for (;;) {
     int cb = 0;
-    if (lane == 0) cb = atomicAdd(p.next_chain, 4);
-    const int cbase = rdl(cb, 0);
-    if (cbase >= p.n_chains) break;
+    if (lane == 0) cb = atomicAdd(p.next_chain, 1);
+    const int u = rdl(cb, 0);
+    if (u >= nq * p.slices) break;
+    const int seg = u / nq;
+    const int quad = u - seg * nq;
+    const uint32_t ustep = (uint32_t)(p.steps * (seg + 1) / p.slices - p.steps * seg / p.slices);
+    if (seg > 0) {
+      // a wave-uniform loop (readfirstlane of the flag): a lane-0-only loop or store lets
+      // the compiler restructure the unit loop around a divergent exit, running the next
+      // unit without lane 0
+      for (;;) {
+        const int done =
+            rfl(__hip_atomic_load(p.seg_done + quad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (done >= seg) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    const int cbase = quad * 4;
     const int c = cbase + row;
     const bool has = c < p.n_chains;
     const int cc = has ? c : cbase;  // a valid index for loads of absent rows
     const uint64_t gid = (uint64_t)(p.chain_id0 + c);
-    const bool cached = p.gcache_ok != 0;  // derived-state cache (FwRunParams)
+    const bool cached = p.gcache_ok != 0 || seg > 0;  // derived-state cache (FwRunParams)
 
     // ---- load state (each row loads its own chain)
     {
@@ -799,7 +824,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       STAMP(-1);
       // ---- who proposes this round
       if (!stuck && (retries >= (uint32_t)p.max_retries || npairs == 0)) stuck = 1;
-      const bool act = has && !stuck && (int64_t)n_steps < p.steps;
+      const bool act = has && !stuck && n_steps < ustep;
       if (ballot(act) == 0ull) break;
 
       if (bpos == ROW) {
@@ -1289,6 +1314,10 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       }
     }
     lds_order();
+    if (seg + 1 < p.slices) {  // hand the quad to its next slice (every lane, one word)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(p.seg_done + quad, seg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   STAMP_FLUSH
 }

@@ -84,6 +84,10 @@ struct FwRunParams {
   // node's neighbourhood (host writes of labels or stats clear gcache_ok)
   int32_t lab_copy16;
   int32_t gcache_ok;
+  // grid kernel work units: quads x slices (fw_grid16_kernel); seg_done [quads] counts a
+  // quad's finished slices (zeroed before a launch with slices > 1)
+  int32_t slices;
+  int32_t* seg_done;
   // spatial observables (nullptr: off).  Per chain c: acc [E] (int64: sum of -t when an
   // edge becomes cut and +t when it becomes uncut, so cut_times = acc + [cut now] * Y),
   // nf / lf [n] (num_flips, last_flipped of finished runs), ps [n] (part_sum), and the

@@ -428,14 +428,22 @@ def test_chain_kernel_3bit_labels(gpu_lib, name, search, monkeypatch):
     assert st["bfs_runs"].sum() > 0
 
 
-@pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("sec11_a2_k2", "auto"),
-                                       ("grid16x24_k8", "auto"), ("grid20_k4_mu", "wave64")])
-def test_many_units_per_wave(gpu_lib, name, path, monkeypatch):
+@pytest.mark.parametrize("name,path,slices", [("grid20_k4_mu", "auto", None), ("sec11_a2_k2", "auto", None),
+                                              ("grid16x24_k8", "auto", None), ("grid20_k4_mu", "wave64", None),
+                                              ("grid20_k4_mu", "auto", "1"), ("grid20_k4_mu", "auto", "3"),
+                                              ("grid16x24_k8", "auto", "7"), ("sec11_a2_k2", "auto", "4")])
+def test_many_units_per_wave(gpu_lib, name, path, slices, monkeypatch):
     """FLIPWALK_GRID_CAP=1 leaves one workgroup, so every wave runs many chains (quads)
     one after another through the work counter, and the grid kernel's later launches load
     each chain's group sums from its record (the derived-state cache) instead of deriving
-    them; trajectories and totals equal one oracle run."""
+    them.  With more quads than waves the grid kernel also cuts each quad's steps into
+    slices handed out slice-major (the host's pick, or FLIPWALK_SLICES), every slice
+    waiting for its quad's previous one; trajectories and totals equal one oracle run."""
     monkeypatch.setenv("FLIPWALK_GRID_CAP", "1")
+    if slices:
+        monkeypatch.setenv("FLIPWALK_SLICES", slices)
+    else:
+        monkeypatch.delenv("FLIPWALK_SLICES", raising=False)
     if path == "wave64":
         monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
     else:
