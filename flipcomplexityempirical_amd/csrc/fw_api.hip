@@ -148,7 +148,7 @@ struct fw_chains {
   uint32_t* d_spill = nullptr;
   int32_t* d_next = nullptr;
   uint32_t* d_gscr = nullptr;  // chain kernel, 3-bit labels: search marks
-  int32_t* d_segdone = nullptr;  // grid kernel: finished slices per quad
+  int32_t* d_segdone = nullptr;  // finished slices per work unit (launch_slices)
   uint64_t max_yields = 0;  // upper bound on any chain's yield count (maps need < 2^32)
   bool gcache_ok = false;   // the label records' group sums and the stats' cut / bnodes /
                             // npairs match the labels (FwRunParams::gcache_ok)
@@ -457,6 +457,11 @@ void fw_chains_destroy(fw_chains* c) {
   delete c;
 }
 
+// work units per slice: the grid kernel's quads (four chains per wave), else chains
+static long long slice_units(const fw_chains* c) {
+  return c->p.use16 ? (c->n_chains + 3) / 4 : c->n_chains;
+}
+
 int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* init_labels,
                      int32_t init_per_chain, int32_t proposal_mode, int64_t pop_lo, int64_t pop_hi,
                      const double* thr, int32_t thr_per_chain, uint64_t seed, int64_t chain_id0,
@@ -640,13 +645,11 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.spill = c->d_spill;
   p.next_chain = c->d_next;
   p.slices = 1;
-  if (use16) {
-    if (hipMalloc(&c->d_segdone, sizeof(int32_t) * (size_t)((n_chains + 3) / 4)) != hipSuccess) {
-      fw_chains_destroy(c);
-      return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
-    }
-    p.seg_done = c->d_segdone;
+  if (hipMalloc(&c->d_segdone, sizeof(int32_t) * (size_t)slice_units(c)) != hipSuccess) {
+    fw_chains_destroy(c);
+    return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
   }
+  p.seg_done = c->d_segdone;
   if ((lb == 3 || lb == 5) && !use16) {  // HBM visit marks of the chain kernel's list search
     p.gscr_words = (n + 7) / 8;
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
@@ -660,20 +663,21 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   return FW_OK;
 }
 
-// Slices per quad for a grid-kernel launch of `steps` steps (see fw_grid16_kernel): with
-// more quads than resident waves W, the S in 1..4 that minimises a uniform-duration model
-// of the launch, ceil(nq S / W) / S rounds of whole-quad time plus ~0.6% of a quad's time
-// per extra slice start (measured: three 333-step launches cost 1.2% more than one
-// 1000-step launch net of their tails).  FLIPWALK_SLICES=x forces x (1: whole quads).
-static int grid16_slices(const fw_chains* c, int64_t steps) {
+// Slices per work unit (a quad of the grid kernel, a chain of the chain kernel) for a
+// launch of `steps` steps (see fw_grid16_kernel / fw_run_kernel): with more units than
+// resident waves W, the S in 1..8 that minimises a uniform-duration model of the launch,
+// ceil(nu S / W) / S rounds of whole-unit time plus ~0.6% of a unit's time per extra slice
+// start (measured on the grid kernel: three 333-step launches cost 1.2% more than one
+// 1000-step launch net of their tails).  FLIPWALK_SLICES=x forces x (1: whole units).
+static int launch_slices(const fw_chains* c, int64_t steps) {
   const char* e = getenv("FLIPWALK_SLICES");
   const int force = e && e[0] ? atoi(e) : 0;
-  const long long nq = (c->n_chains + 3) / 4, W = (long long)c->grid * c->p.nw;
+  const long long nq = slice_units(c), W = (long long)c->grid * (c->p.use16 ? c->p.nw : 1);
   if (force >= 1) return (int)std::min<long long>(force, std::max<int64_t>(steps, 1));
   if (nq <= W || steps < 64) return 1;
   int best = 1;
   double best_t = 1e300;
-  for (int S = 1; S <= 4; ++S) {
+  for (int S = 1; S <= 8; ++S) {
     const double rounds = (double)((nq * S + W - 1) / W) / S;
     const double t = rounds + 0.006 * (S - 1) * (double)nq / (double)W;
     if (t < best_t - 1e-9) {
@@ -709,10 +713,9 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
     const int64_t s = left < cap ? left : cap;
     c->p.steps = s;
     c->p.gcache_ok = c->gcache_ok ? 1 : 0;
-    c->p.slices = c->p.use16 && !c->p.trace ? grid16_slices(c, s) : 1;
+    c->p.slices = !c->p.trace ? launch_slices(c, s) : 1;
     if (c->p.slices > 1)
-      HIPCHK(hipMemsetAsync(c->d_segdone, 0, sizeof(int32_t) * (size_t)((c->n_chains + 3) / 4),
-                            c->stream));
+      HIPCHK(hipMemsetAsync(c->d_segdone, 0, sizeof(int32_t) * (size_t)slice_units(c), c->stream));
     HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));
     const int le = fw_launch_run(c->p, c->lb, c->grid, c->stream);
     if (le != 0) {

@@ -29,6 +29,21 @@
 #ifdef FW_STAMPS
 // Diagnostic build only (libflipwalk_stamps.so): per-phase s_memtime shares.
 __device__ unsigned long long g_stamps[16];
+// per work unit: s_memrealtime (100 MHz) at its start and at its write-back (units < 2^16)
+// and where it ran: HW_ID (wave slot, SIMD, CU, SA, SE) | XCC_ID << 32
+__device__ unsigned long long g_unit_t[2 * 65536];
+__device__ unsigned long long g_unit_hw[65536];
+#define UNIT_TIME(u, e)                                                         \
+  do {                                                                          \
+    uint64_t t_;                                                                \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    if (__lane_id() == 0 && (u) < 65536) {                                      \
+      g_unit_t[2 * (u) + (e)] = t_;                                             \
+      if ((e) == 0)                                                             \
+        g_unit_hw[u] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) | \
+                       ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32); \
+    }                                                                           \
+  } while (0)
 #define STAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_t0 = 0;
 #define STAMP(i)                                              \
   do {                                                        \
@@ -48,6 +63,7 @@ __device__ unsigned long long g_stamps[16];
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_FLUSH
+#define UNIT_TIME(u, e)
 #endif
 
 #include <cstddef>
@@ -650,6 +666,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
+    UNIT_TIME(u, 0);
     const int cbase = quad * 4;
     const int c = cbase + row;
     const bool has = c < p.n_chains;
@@ -820,12 +837,30 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     int bpos = ROW;
 
     const bool unit_pop = p.g.pop == nullptr;
+    // Wave priority by progress.  A SIMD issues VALU to the higher-priority wave, then the
+    // older one: at equal priority the younger waves of a SIMD get the leftover slots and
+    // finish their units ~25% later (8,192 chains, 2 waves per SIMD: 2.38 vs 3.01 ms,
+    // scripts/unit_times.py), and with no more units to take the launch waits for them.
+    // Priority 3 - (level mod 4), the level counting 32nds of the unit's steps done by
+    // row 0, hands the issue slots to the wave one level behind (except across a wrap),
+    // which keeps a SIMD's waves within about one level of each other to the end.
+    const uint32_t pstep = ustep >= 64u ? ustep >> 5 : 2u;
+    uint32_t pnext = pstep, plev = 0;
+    __builtin_amdgcn_s_setprio(3);
     for (;;) {
       STAMP(-1);
       // ---- who proposes this round
       if (!stuck && (retries >= (uint32_t)p.max_retries || npairs == 0)) stuck = 1;
       const bool act = has && !stuck && n_steps < ustep;
       if (ballot(act) == 0ull) break;
+      if (rfl(n_steps) >= pnext) {
+        pnext += pstep;
+        plev = (plev + 1u) & 3u;
+        if (plev == 0) __builtin_amdgcn_s_setprio(3);
+        else if (plev == 1) __builtin_amdgcn_s_setprio(2);
+        else if (plev == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
 
       if (bpos == ROW) {
         if (n_sdeg >= p.fold_at) {  // rare: fold (see att0); one row at a time
@@ -1314,6 +1349,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       }
     }
     lds_order();
+    UNIT_TIME(u, 1);
     if (seg + 1 < p.slices) {  // hand the quad to its next slice (every lane, one word)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __hip_atomic_store(p.seg_done + quad, seg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1365,6 +1401,14 @@ int round16i(int x) { return (x + 15) / 16 * 16; }
 }  // namespace
 
 #ifdef FW_STAMPS
+extern "C" int fw_debug_unit_times(unsigned long long* out, int n) {
+  if (n > 65536) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_unit_t), sizeof(unsigned long long) * 2 * n) !=
+      hipSuccess)
+    return -1;
+  return hipMemcpyFromSymbol(out + 2 * n, HIP_SYMBOL(g_unit_hw), sizeof(unsigned long long) * n) ==
+                 hipSuccess ? 0 : -1;
+}
 extern "C" int fw_debug_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
     return -1;

@@ -83,16 +83,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   __shared__ int32_t s_chain;
   CSTAMP_DECL
 
+  // Work units: chain x slice of the launch's steps, handed out slice-major (unit u =
+  // slice u / n_chains of chain u % n_chains; p.slices = 1: whole chains), as in
+  // fw_grid16_kernel: with more chains than resident waves the host picks the slice count
+  // that ends the launch on a full residency round (C5 shard: 8,192 chains x 5 = 16 rounds
+  // of 2,560 waves instead of 3.2).  A slice waits for its chain's previous one (seg_done,
+  // agent-scope release / acquire); the trajectory equals separate launches of the slices.
   for (;;) {
     if (lane == 0) s_chain = atomicAdd(p.next_chain, 1);
     __syncthreads();
-    const int c = rfl(s_chain);
-    if (c >= p.n_chains) break;
+    const int u = rfl(s_chain);
+    if (u >= p.n_chains * p.slices) break;
+    const int seg = u / p.n_chains;
+    const int c = u - seg * p.n_chains;
+    const int64_t ustep = p.steps * (seg + 1) / p.slices - p.steps * seg / p.slices;
+    if (seg > 0) {
+      for (;;) {
+        const int done =
+            rfl(__hip_atomic_load(p.seg_done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (done >= seg) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
     const uint64_t gid = (uint64_t)(p.chain_id0 + c);
 
     // ---- load state (with a valid derived-state cache the group sums that follow the
     // labels in the chain's record come along: FwRunParams::lab_copy16)
-    const bool cached = p.gcache_ok != 0;
+    const bool cached = p.gcache_ok != 0 || seg > 0;
     {
       const u32x4* src = reinterpret_cast<const u32x4*>(p.labels + (size_t)c * p.lab_stride);
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(C.lab);
@@ -205,7 +223,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     int bpos = WAVE;
 
     const bool unit_pop = p.g.pop == nullptr;
-    for (int64_t s = 0; s < p.steps && !stuck; ++s) {
+    // wave priority 3 - (level mod 4), the level counting 32nds of the unit's steps: the
+    // SIMD's VALU goes to the wave one level behind instead of the oldest (see
+    // fw_grid16_kernel), so the waves of the last residency round finish together
+    const int64_t pstep = ustep >= 64 ? ustep >> 5 : 2;
+    int64_t pnext = pstep;
+    uint32_t plev = 0;
+    __builtin_amdgcn_s_setprio(3);
+    for (int64_t s = 0; s < ustep && !stuck; ++s) {
+      if (s >= pnext) {
+        pnext += pstep;
+        plev = (plev + 1u) & 3u;
+        if (plev == 0) __builtin_amdgcn_s_setprio(3);
+        else if (plev == 1) __builtin_amdgcn_s_setprio(2);
+        else if (plev == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
       int32_t retries = 0;
       int v = 0, dcut = 0, m = 0, nbd = 0, dv = 0;
       uint32_t a = 0, d = 0;
@@ -413,6 +446,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       stp->bnodes = bnodes;
       stp->npairs = npairs;
       stp->stuck = stuck;
+    }
+    if (seg + 1 < p.slices) {  // hand the chain to its next slice
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every lane, one word
+      __hip_atomic_store(p.seg_done + c, seg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
   }
