@@ -673,11 +673,13 @@ static int launch_slices(const fw_chains* c, int64_t steps) {
   const char* e = getenv("FLIPWALK_SLICES");
   const int force = e && e[0] ? atoi(e) : 0;
   const long long nq = slice_units(c), W = (long long)c->grid * (c->p.use16 ? c->p.nw : 1);
-  if (force >= 1) return (int)std::min<long long>(force, std::max<int64_t>(steps, 1));
+  // the kernels number units in int32: nq * S stays below 2^31
+  const long long s_max = std::max<long long>(1, std::min<long long>(8, 0x7FFFFFFFll / std::max(nq, 1ll)));
+  if (force >= 1) return (int)std::min<long long>({(long long)force, std::max<int64_t>(steps, 1), s_max});
   if (nq <= W || steps < 64) return 1;
   int best = 1;
   double best_t = 1e300;
-  for (int S = 1; S <= 8; ++S) {
+  for (int S = 1; S <= s_max; ++S) {
     const double rounds = (double)((nq * S + W - 1) / W) / S;
     const double t = rounds + 0.006 * (S - 1) * (double)nq / (double)W;
     if (t < best_t - 1e-9) {
