@@ -428,20 +428,24 @@ def test_chain_kernel_3bit_labels(gpu_lib, name, search, monkeypatch):
     assert st["bfs_runs"].sum() > 0
 
 
-@pytest.mark.parametrize("name,path,slices", [("grid20_k4_mu", "auto", None), ("sec11_a2_k2", "auto", None),
-                                              ("grid16x24_k8", "auto", None), ("grid20_k4_mu", "wave64", None),
-                                              ("grid20_k4_mu", "auto", "1"), ("grid20_k4_mu", "auto", "3"),
-                                              ("grid16x24_k8", "auto", "7"), ("sec11_a2_k2", "auto", "4"),
-                                              ("grid20_k4_mu", "wave64", "3"), ("tract_k4", "auto", "5")])
-def test_many_units_per_wave(gpu_lib, name, path, slices, monkeypatch):
-    """FLIPWALK_GRID_CAP=1 leaves one workgroup, so every wave runs many chains (quads)
+@pytest.mark.parametrize("name,path,slices,cap", [
+    ("grid20_k4_mu", "auto", None, "1"), ("sec11_a2_k2", "auto", None, "1"),
+    ("grid16x24_k8", "auto", None, "1"), ("grid20_k4_mu", "wave64", None, "1"),
+    ("grid20_k4_mu", "auto", "1", "1"), ("grid20_k4_mu", "auto", "3", "1"),
+    ("grid16x24_k8", "auto", "7", "1"), ("sec11_a2_k2", "auto", "4", "1"),
+    ("grid20_k4_mu", "wave64", "3", "1"), ("tract_k4", "auto", "5", "1"),
+    # several waves: a slice waits on its unit's previous slice held by another wave
+    ("grid20_k4_mu", "auto", "3", "2"), ("sec11_a2_k2", "auto", "4", "3"),
+    ("tract_k4", "auto", "6", "5")])
+def test_many_units_per_wave(gpu_lib, name, path, slices, cap, monkeypatch):
+    """FLIPWALK_GRID_CAP=1 leaves one workgroup (more: a few), so every wave runs many chains (quads)
     one after another through the work counter, and the grid kernel's later launches load
     each chain's group sums from its record (the derived-state cache) instead of deriving
     them.  With more work units than waves both kernels also cut each unit's steps (a quad
     of the grid kernel, a chain of the chain kernel) into slices handed out slice-major
     (the host's pick, or FLIPWALK_SLICES), every slice waiting for its unit's previous one;
     trajectories and totals equal one oracle run."""
-    monkeypatch.setenv("FLIPWALK_GRID_CAP", "1")
+    monkeypatch.setenv("FLIPWALK_GRID_CAP", cap)
     if slices:
         monkeypatch.setenv("FLIPWALK_SLICES", slices)
     else:
