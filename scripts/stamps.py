@@ -13,7 +13,8 @@ from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bo
 
 L = _lib.load()
 L.fw_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-# usage: stamps.py [config] [chains]   (config c3 default; c5 = the 64-base ladder workload)
+# usage: stamps.py [config] [chains] [warm launches]   (config c3 default; c5 = the 64-base
+# ladder workload; warm launches of 1000 steps before the stamped ones, default 2)
 from flipcomplexityempirical_amd.workloads import workload  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 w = workload(cfg)
@@ -22,8 +23,8 @@ g = w.graph
 dg = DeviceGraph(g)
 ch = Chains(dg, nch, w.k, w.init, proposal=w.proposal,
             pop_bounds=population_bounds(g.total_pop, w.k, w.percent), base=w.bases(0, nch), seed=0)
-ch.run(1000)
-ch.run(1000)
+for _ in range(int(sys.argv[3]) if len(sys.argv) > 3 else 2):
+    ch.run(1000)
 buf = np.zeros(16, np.uint64)
 L.fw_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), 1)
 L.fw_debug_stamps_csr.argtypes = [ctypes.c_void_p, ctypes.c_int]
