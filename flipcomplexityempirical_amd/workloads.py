@@ -32,18 +32,22 @@ def ladder(n_bases: int = 64, lo: float = 0.1, hi: float = 10.0) -> np.ndarray:
 
 def ladder_base_index(cid, n_bases: int = 64, n_gpus_hint: int = 8,
                       interleave: bool = True) -> np.ndarray:
-    """Ladder index of global chain id(s) ``cid``: base group b = cid // 1024 runs ladder
-    entry (b % 8) * 8 + b // 8.  Every 8,192-id block (one GPU's shard at 8 GPUs) thus
-    holds 8 whole base groups spread over the ladder (entries r, r+8, ..., r+56) instead
-    of 8 adjacent ones: the low bases, whose fractal boundaries make steps several times
-    dearer, are not all on one GPU.  A fixed function of the id, independent of the GPU
-    count."""
+    """Ladder index of global chain id(s) ``cid``: base group b = cid // 1024 of block
+    s = b // 8 (one GPU's 8,192-id shard at 8 GPUs) runs, at position i = b % 8, an entry
+    of ladder octave i: 8 i + s for even i, 8 i + 7 - s for odd i.  Every shard thus holds
+    8 whole base groups spread over the ladder, and the snake order gives every shard the
+    same mix of cheap and dear bases (the low bases grow fractal boundaries that make steps
+    several times dearer; adjacent groups put them all on one GPU, and the plain
+    interleave 8 i + s still left shard 0 with the lowest base of every octave: 0.39 vs
+    0.44 x 10^9 flip steps/s for shard 7, profiles/r02/round_d/shards_c5_n8.jsonl).
+    A fixed function of the id, independent of the GPU count."""
     b = np.asarray(cid, np.int64) // LADDER_GROUP
     per = n_bases // n_gpus_hint
     b = b % n_bases
     if not interleave:  # round 1's assignment: adjacent groups, ladder entry b
         return b
-    return (b % per) * n_gpus_hint + b // per
+    i, s = b % per, b // per
+    return i * n_gpus_hint + np.where(i % 2 == 0, s, n_gpus_hint - 1 - s)
 
 
 @dataclass
