@@ -24,6 +24,9 @@ done
 timeout -k 10 300 python -u bench.py --config c5 --shard 0/8 --ladder contiguous --steps 5 --warmup 1 \
     --no-cpu-baseline > $O/bench_c5_r01protocol.json 2> $O/bench_configs.err || { echo "c5 r01 protocol failed"; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench_c5_r01protocol.json').read().splitlines()[-1]); print('c5 contiguous shard 0, r01 protocol', '%.4g' % d['value'])"
+# the driver's own protocol (BENCH_r01.json: --steps 20 --warmup 5)
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_c3_driver.json 2> $O/bench_configs.err || { echo "c3 driver protocol failed"; exit 1; }
+python3 -c "import json; d=json.loads(open('$O/bench_c3_driver.json').read().splitlines()[-1]); print('c3 driver protocol 20/5', '%.4g' % d['value'])"
 # SURVEY 8d's steady-state protocol: 10^4 warm-up steps, then 10^5 timed, per chain
 timeout -k 10 300 python -u bench.py --warmup 10 --steps 100 --no-cpu-baseline > $O/bench_c3_steady.json 2> $O/bench_configs.err || { echo "c3 steady failed"; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench_c3_steady.json').read().splitlines()[-1]); print('c3 steady state', '%.4g' % d['value'])"
