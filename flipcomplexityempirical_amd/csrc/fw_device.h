@@ -531,12 +531,16 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
 }
 
 // Level-1 group sums of the one-chain-per-wave kernel: lane l owns groups l*PER .. l*PER +
-// PER-1, stored at l*(PER+1) + t.  The pad word per lane makes the PER per-lane reads of a
-// select conflict-free (lane stride PER+1 is odd: 32 distinct banks per 32-lane group;
-// without it, stride 16 put the 32 lanes of a ds_read_b32 group on 2 banks).
+// PER-1 (PER even), stored as u16 pairs in dwords l*SD .. l*SD + PER/2 - 1, so a select
+// reads them with PER/2 dword loads.  The lane stride SD (PER/2, padded to the next odd
+// number) keeps those loads conflict-free: 32 distinct banks per 32-lane group (stride 8
+// put the 32 lanes of a ds_read_b32 group on 4 banks).
+__host__ __device__ constexpr int gsum_stride_dw(int per) {
+  return (per / 2) % 2 ? per / 2 : per / 2 + 1;
+}
 template <int PER>
 __device__ __forceinline__ int gsum_slot(int g) {
-  return (g / PER) * (PER + 1) + (g % PER);
+  return (g / PER) * (2 * gsum_stride_dw(PER)) + (g % PER);
 }
 
 // E16: a general graph of max degree <= 16 whose adjacency rows are read from the padded
@@ -775,15 +779,19 @@ struct Ctx {
   // PER = group sums held per lane (compile-time bound, >= ceil(G/64)).
   template <int MODE, int PER>
   __device__ __forceinline__ void select(uint32_t r, int G, int& v, uint32_t& j) const {
+    static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
+    constexpr int SD = gsum_stride_dw(PER);
     uint32_t gs[PER];
     uint32_t s = 0;
     const int g0 = lane * PER;
-    const int slot_last = gsum_slot<PER>(G - 1);
+    const int dw_last = gsum_slot<PER>(G - 1) >> 1;
+    const LDS uint32_t* g32 = reinterpret_cast<const LDS uint32_t*>(gsum);
 #pragma unroll
-    for (int t = 0; t < PER; ++t) {  // unconditional (clamped) reads, masked values
-      const uint32_t w = gsum[min(lane * (PER + 1) + t, slot_last)];
-      gs[t] = g0 + t < G ? w : 0u;
-      s += gs[t];
+    for (int t = 0; t < PER / 2; ++t) {  // unconditional (clamped) u16-pair reads, masked values
+      const uint32_t w = g32[min(lane * SD + t, dw_last)];
+      gs[2 * t] = g0 + 2 * t < G ? (w & 0xFFFFu) : 0u;
+      gs[2 * t + 1] = g0 + 2 * t + 1 < G ? (w >> 16) : 0u;
+      s += gs[2 * t] + gs[2 * t + 1];
     }
     const uint32_t incl = scan_incl(s);
     const uint64_t m = ballot(incl > r);

@@ -592,10 +592,12 @@ extern "C" int fw_debug_stamps_csr(unsigned long long* out, int reset) {
 
 // group sums per lane of the one-chain-per-wave kernel (pick_per) and the u16 LDS slots
 // its padded level-1 layout (gsum_slot) takes for G groups
-int fw_run_per(int G) { return G <= 64 * 2 ? 2 : G <= 64 * 4 ? 4 : G <= 64 * 8 ? 8 : 16; }
+int fw_run_per(int G) {
+  return G <= 64 * 2 ? 2 : G <= 64 * 4 ? 4 : G <= 64 * 8 ? 8 : G <= 64 * 10 ? 10 : 16;
+}
 int fw_run_gsum_slots(int G) {
   const int per = fw_run_per(G);
-  return G <= 0 ? 0 : ((G - 1) / per) * (per + 1) + (G - 1) % per + 1;
+  return G <= 0 ? 0 : ((G - 1) / per) * (2 * gsum_stride_dw(per)) + (G - 1) % per + 1;
 }
 
 namespace {
@@ -606,6 +608,7 @@ void* pick_per(int G) {
     case 2: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE>);
     case 4: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE>);
     case 8: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE>);
+    case 10: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 10, E16, WPE>);
     default: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE>);
   }
 }
