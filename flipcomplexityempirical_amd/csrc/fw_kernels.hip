@@ -58,7 +58,9 @@ namespace {
 
 // ---------------------------------------------------------------- the chain kernel
 // WPE: waves per SIMD the register budget targets (5 only where LDS admits 20 chains per CU)
-template <int LB, bool GRID, int MODE, int PER, bool E16, int WPE = 4>
+// FULL = false: the lean instantiation for the common configuration (cut_accept, no
+// spatial maps, ring observable, bound schedule or trace), as in fw_grid16_kernel
+template <int LB, bool GRID, int MODE, int PER, bool E16, int WPE = 4, bool FULL = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void fw_run_kernel(FwRunParams p) {
   extern __shared__ __align__(16) uint8_t smem[];
   Ctx<LB, GRID, E16> C;
@@ -120,14 +122,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     int64_t pops = lane < k ? p.pops[(size_t)c * k + lane] : 0;  // lane d holds district d
     double thr_l = lane < 2 * D + 1 ? p.thr[(size_t)c * p.thr_stride + lane] : 0.0;
     fw_chain_stats* stp = p.stats + c;
-    const uint64_t acc0 = p.sched ? rfl64(stp->accepts) : 0ull;
+    const uint64_t acc0 = FULL && p.sched ? rfl64(stp->accepts) : 0ull;
     // scheduled bounds: the row of the next proposal's step_num (accepted flips + 1)
     auto sched_row = [&](uint64_t nacc) {
       const int64_t t = (int64_t)(acc0 + nacc) + 1 - p.sched_t0;
       const int64_t r = t < 0 ? 0 : (t >= p.sched_rows ? p.sched_rows - 1 : t);
       if (lane < 2 * D + 1) thr_l = p.sched[r * (2 * D + 1) + lane];
     };
-    if (p.sched) sched_row(0);
+    if (FULL && p.sched) sched_row(0);
     uint64_t attempts = rfl64(stp->attempts);
     const uint64_t yields0 = rfl64(stp->yields);
     int32_t stuck = rfl(stp->stuck);
@@ -139,9 +141,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     uint32_t n_steps = in_vgpr(0), n_acc = in_vgpr(0), n_popf = in_vgpr(0), n_conf = in_vgpr(0);
     uint32_t n_sdeg = in_vgpr(0), n_adeg = in_vgpr(0), n_bchg = in_vgpr(0), n_yield = in_vgpr(0);
     uint64_t n_bfs = in_vgpr64(0), n_bfsn = in_vgpr64(0), n_bfsd = in_vgpr64(0);
-    Pend pend = pend_load(p, c);
+    Pend pend = FULL ? pend_load(p, c) : Pend{-1, 0, 0u};
     // boundary_node-flagged nodes of district `lane` (FW_ACCEPT_BOUNDARY)
-    int32_t bcnt = p.accept == FW_ACCEPT_BOUNDARY && lane < k ? p.bcnt[(size_t)c * k + lane] : 0;
+    int32_t bcnt = FULL && p.accept == FW_ACCEPT_BOUNDARY && lane < k ? p.bcnt[(size_t)c * k + lane] : 0;
     __syncthreads();
 
     // ---- derive group sums, cut count, boundary count, proposal-set size (unless cached)
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // district-shape observable: the pair of the first two cut ring edges (ring order),
     // counted per yield in runs (a pair changes only when an accepted flip moves a ring
     // node), flushed to the ring histogram when it changes and at the end of the launch
-    const int RN = p.ring_n;
+    const int RN = FULL ? p.ring_n : 0;
     auto ring_pair = [&]() -> int32_t {  // wave-uniform; labels must be clean (no search marks)
       int f = -1, sc = -1;
       for (int b0 = 0; b0 < RN && sc < 0; b0 += WAVE) {
@@ -343,18 +345,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const int minus = __popcll(ballot(mine && wo > 0 && wn == 0));
       // ---- accept rule (include/flipwalk.h FW_ACCEPT_*)
       bool accepted;
-      if (p.accept == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
+      if (FULL && p.accept == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
         const int32_t fv = p.flags[v] ? 1 : 0;
         const int32_t cnt = bcnt - (lane == (int)a ? fv : 0) + (lane == (int)d ? fv : 0);
         accepted = __popcll(ballot(lane < k && cnt > 0)) >= 2;
       } else {  // cut_accept (grid_chain_sec11.py:171-179) [* |B'|/|B|, :81-110]
         double bound = rdl_f64(thr_l, dcut + D);
-        if (p.accept == FW_ACCEPT_BRATIO)
+        if (FULL && p.accept == FW_ACCEPT_BRATIO)
           bound = bound * ((double)(bnodes + plus - minus) / (double)bnodes);
         accepted = u53(x.x2, x.x3) < bound;
       }
-      if (p.trace && lane == 0) p.trace[(size_t)c * p.steps + s] = accepted ? v * 64 + (int)d : -1;
-      if (accepted && p.m_acc != nullptr) {  // spatial observables: fire-and-forget atomics
+      if (FULL && p.trace && lane == 0) p.trace[(size_t)c * p.steps + s] = accepted ? v * 64 + (int)d : -1;
+      if (FULL && accepted && p.m_acc != nullptr) {  // spatial observables: fire-and-forget atomics
         const int64_t t = (int64_t)(yields0 + n_yield);  // index of the new state's yield
         const bool nbl = GRID ? (lane >= 1 && lane <= 4 && h.x >= 0) : (lane >= 1 && lane <= dv);
         if (nbl && (h.lx == a || h.lx == d)) {
@@ -377,7 +379,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       if (accepted) {
         n_acc += 1;
-        if (p.sched) sched_row(n_acc);
+        if (FULL && p.sched) sched_row(n_acc);
         n_adeg += (uint32_t)dv;
         if (lane == 0) PK<LB>::axor(C.lab, v, a ^ d);
         if (mine && h.x >= 0 && wn != wo) {
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (plus | minus) invb = 1.0 / (double)max(bnodes, 1);
         if (lane == (int)a) pops -= pv;
         if (lane == (int)d) pops += pv;
-        if (p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
+        if (FULL && p.accept == FW_ACCEPT_BOUNDARY && p.flags[v]) {
           if (lane == (int)a) bcnt -= 1;
           if (lane == (int)d) bcnt += 1;
         }
@@ -423,9 +425,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(C.lab);
       for (int i = lane; i < p.lab_copy16; i += WAVE) dst[i] = src[i];  // labels + group sums
       if (lane < k) p.pops[(size_t)c * k + lane] = pops;
-      if (lane < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lane] = bcnt;
+      if (FULL && lane < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lane] = bcnt;
     }
-    if (lane == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
+    if (FULL && lane == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
     if (lane == 0) {
       stp->attempts = attempts;
       stp->steps += n_steps;
@@ -602,38 +604,45 @@ int fw_run_gsum_slots(int G) {
 
 namespace {
 
-template <int LB, bool GRID, int MODE, bool E16, int WPE = 4>
+template <int LB, bool GRID, int MODE, bool E16, int WPE = 4, bool FULL = true>
 void* pick_per(int G) {
   switch (fw_run_per(G)) {
-    case 2: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE>);
-    case 4: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE>);
-    case 8: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE>);
-    case 10: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 10, E16, WPE>);
-    default: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE>);
+    case 2: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE, FULL>);
+    case 4: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE, FULL>);
+    case 8: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE, FULL>);
+    case 10: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 10, E16, WPE, FULL>);
+    default: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE, FULL>);
   }
 }
 
-// grids: implicit neighbours; general graphs: the padded 16-wide table when it exists
-void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false) {
+template <bool FULL>
+void* pick_run_t(int lb, bool grid, bool e16, int mode, int G, bool wpe5) {
   const bool cut = mode == FW_PROPOSE_CUTEDGE;
   if (lb == 4) {
     // small general graphs (4-bit labels, padded rows): a 5-waves-per-SIMD register budget
     if (!grid && e16 && wpe5)
-      return cut ? pick_per<4, false, 2, true, 5>(G) : pick_per<4, false, 1, true, 5>(G);
-    if (grid) return cut ? pick_per<4, true, 2, false>(G) : pick_per<4, true, 1, false>(G);
-    if (e16) return cut ? pick_per<4, false, 2, true>(G) : pick_per<4, false, 1, true>(G);
-    return cut ? pick_per<4, false, 2, false>(G) : pick_per<4, false, 1, false>(G);
+      return cut ? pick_per<4, false, 2, true, 5, FULL>(G) : pick_per<4, false, 1, true, 5, FULL>(G);
+    if (grid) return cut ? pick_per<4, true, 2, false, 4, FULL>(G) : pick_per<4, true, 1, false, 4, FULL>(G);
+    if (e16) return cut ? pick_per<4, false, 2, true, 4, FULL>(G) : pick_per<4, false, 1, true, 4, FULL>(G);
+    return cut ? pick_per<4, false, 2, false, 4, FULL>(G) : pick_per<4, false, 1, false, 4, FULL>(G);
   }
   if (lb == 5)  // general graphs with padded rows, 16 <= k <= 31 (fw_chains_create)
-    return !grid && e16 ? (wpe5 ? (cut ? pick_per<5, false, 2, true, 5>(G) : pick_per<5, false, 1, true, 5>(G))
-                                : (cut ? pick_per<5, false, 2, true>(G) : pick_per<5, false, 1, true>(G)))
+    return !grid && e16 ? (wpe5 ? (cut ? pick_per<5, false, 2, true, 5, FULL>(G) : pick_per<5, false, 1, true, 5, FULL>(G))
+                                : (cut ? pick_per<5, false, 2, true, 4, FULL>(G) : pick_per<5, false, 1, true, 4, FULL>(G)))
                         : nullptr;
   if (lb == 3)  // grids, k <= 8 (the large-grid LDS plan: fw_chains_create)
-    return grid ? (cut ? pick_per<3, true, 2, false, 3>(G) : pick_per<3, true, 1, false, 3>(G))
+    return grid ? (cut ? pick_per<3, true, 2, false, 3, FULL>(G) : pick_per<3, true, 1, false, 3, FULL>(G))
                 : nullptr;  // <= 3 waves per SIMD: LDS holds 9 chains per CU
-  if (grid) return cut ? pick_per<8, true, 2, false>(G) : pick_per<8, true, 1, false>(G);
-  if (e16) return cut ? pick_per<8, false, 2, true>(G) : pick_per<8, false, 1, true>(G);
-  return cut ? pick_per<8, false, 2, false>(G) : pick_per<8, false, 1, false>(G);
+  if (grid) return cut ? pick_per<8, true, 2, false, 4, FULL>(G) : pick_per<8, true, 1, false, 4, FULL>(G);
+  if (e16) return cut ? pick_per<8, false, 2, true, 4, FULL>(G) : pick_per<8, false, 1, true, 4, FULL>(G);
+  return cut ? pick_per<8, false, 2, false, 4, FULL>(G) : pick_per<8, false, 1, false, 4, FULL>(G);
+}
+
+// grids: implicit neighbours; general graphs: the padded 16-wide table when it exists.
+// The LDS plan and residency are sized on the FULL instantiation (the optional features
+// can be switched on after fw_chains_create); launches take the lean one when they are off.
+void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false, bool full = true) {
+  return full ? pick_run_t<true>(lb, grid, e16, mode, G, wpe5) : pick_run_t<false>(lb, grid, e16, mode, G, wpe5);
 }
 
 }  // namespace
@@ -708,7 +717,9 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
 
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   if (p.use16) return fw_grid16_launch(p, grid, stream);
-  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0);
+  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
+                    p.ring_n > 0 || p.trace != nullptr;
+  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0, full);
   // handles of different graphs share instantiations: set this handle's LDS size
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   if (e != hipSuccess) return (int)e;
