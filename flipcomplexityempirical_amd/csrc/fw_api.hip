@@ -493,14 +493,19 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     if (!use16 && g->gw > 0 && k <= 8 && lb == 4 && (want == 3 || (want == 0 && G > 256)))
       lb = 3;
     // general graphs on padded rows whose k + maxdeg needs 8-bit in-place codes: 5-bit
-    // labels with the marks in HBM once the labels dominate LDS (n > 16,384: 8-bit labels
-    // would hold fewer than 10 chains per CU).  C4 (9,000 nodes, k = 18) keeps 8 bits: 5 bits
-    // there reach 20 chains per CU only with the 5-wave register budget, which spills
-    // (0.495 vs 0.523 x 10^9, profiles/r02/ab/csr_5bit_c4.jsonl).  FLIPWALK_CSR_LB=5 / 8
-    // forces / forbids (5 also for k <= 15).
-    if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 &&
-        (want == 5 || (want == 0 && lb == 8 && n > 16384)))
-      lb = 5;
+    // labels with the list search's marks in HBM when that fits more chains per CU — the
+    // 8-bit plan is held to 16 by the 4-waves-per-SIMD register budget, the 5-bit one to 20
+    // by the 5-wave budget of the lean kernel (C4, 9,000 nodes, k = 18: 16 -> 20 chains per
+    // CU, 0.576 -> 0.588 x 10^9; before the lean instantiation the 5-wave budget spilled,
+    // 0.495 vs 0.523, profiles/r02/ab/csr_5bit_c4.jsonl).  FLIPWALK_CSR_LB=5 / 8 forces /
+    // forbids (5 also for k <= 15).
+    if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 && lb == 8 && want == 0) {
+      const long long gs = round16((int64_t)fw_run_gsum_slots(G) * 2), lds = 160 * 1024;
+      const long long l8 = round16(((int64_t)n * 8 + 7) / 8 + 8) + gs + 4 * 128;
+      const long long l5 = round16(((int64_t)n * 5 + 7) / 8 + 8) + gs + 4 * 8;
+      if (n > 16384 || std::min(20ll, lds / l5) > std::min(16ll, lds / l8)) lb = 5;
+    }
+    if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 && want == 5) lb = 5;
   }
   if (!lb) return fail(FW_EUNSUPPORTED, "k + maxdeg = %d too large", k + g->maxdeg);
 

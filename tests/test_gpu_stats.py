@@ -226,8 +226,8 @@ def _oracle_rerun(g, init, k, mode, bounds, thr, seed, cid, steps_list):
 
 def test_c4_full_size_properties(gpu_lib):
     """BASELINE configs[3] at its stated size: the 9,000-node Delaunay dual graph, k=18 tree
-    seed, 16,384 chains, with the production LDS plan the host picks for it (160-entry
-    visit list + HBM spill, 16 chains per CU; no FLIPWALK_* overrides)."""
+    seed, 16,384 chains, with the production LDS plan the host picks for it (5-bit labels,
+    list-search marks in HBM, 20 chains per CU; no FLIPWALK_* overrides)."""
     from flipcomplexityempirical_amd.workloads import workload
     for var in ("FLIPWALK_LIST_CAP", "FLIPWALK_NO_BITBOARD", "FLIPWALK_NO_GRID16"):
         assert var not in os.environ
