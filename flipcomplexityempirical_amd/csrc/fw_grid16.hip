@@ -1240,7 +1240,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         accepted = valid & (((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u) != 0u);
       }
       STAMP(8);  // outcome, accept rule
-      if (p.trace != nullptr && valid && q == 0)
+      if (FULL && p.trace != nullptr && valid && q == 0)
         p.trace[(size_t)c * p.steps + n_steps] = accepted ? v * 64 + (int)d : -1;
       n_steps += valid ? 1u : 0u;
       if (maps_on && accepted) {  // spatial observables: fire-and-forget atomics
@@ -1441,7 +1441,7 @@ int fw_grid16_lb(int G, int k) { return k <= 4 ? 2 : (is_big(G) ? 3 : 4); }
 
 void* fw_grid16_fn(const FwRunParams& p) {
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
-                    p.ring_n > 0;
+                    p.ring_n > 0 || p.trace != nullptr;
   return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
 }
 
