@@ -836,7 +836,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     U4 pb = {0u, 0u, 0u, 0u};
     int bpos = ROW;
 
-    const bool unit_pop = p.g.pop == nullptr;
+    const bool unit_pop = !FULL || p.g.pop == nullptr;  // node populations: FULL only
     // Wave priority by progress.  A SIMD issues VALU to the higher-priority wave, then the
     // older one: at equal priority the younger waves of a SIMD get the leftover slots and
     // finish their units ~25% later (8,192 chains, 2 waves per SIMD: 2.38 vs 3.01 ms,
@@ -1441,7 +1441,7 @@ int fw_grid16_lb(int G, int k) { return k <= 4 ? 2 : (is_big(G) ? 3 : 4); }
 
 void* fw_grid16_fn(const FwRunParams& p) {
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
-                    p.ring_n > 0 || p.trace != nullptr;
+                    p.ring_n > 0 || p.trace != nullptr || p.g.pop != nullptr;
   return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
 }
 
