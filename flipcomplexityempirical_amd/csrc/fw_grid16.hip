@@ -1066,6 +1066,34 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const bool pop_ok = rowbits(ballot(bad), row) == 0u;
 
       STAMP(3);  // gather, target, Δcut, population
+      // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
+      uint32_t wo = 0, wn = 0;
+      const bool mine = (q <= 4) & (h.x >= 0);
+      // branch-free (selects, no exec-mask if/else between v's lane and its neighbours')
+      if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
+        const uint32_t wo_v = (uint32_t)(h.deg - m), wn_v = (uint32_t)(h.deg - nbd);
+        const uint32_t wo_u = h.cnt + (uint32_t)(h.has_v & (a != h.lx));
+        const uint32_t wn_u = h.cnt + (uint32_t)(h.has_v & (d != h.lx));
+        wo = q == 0 ? wo_v : wo_u;
+        wn = q == 0 ? wn_v : wn_u;
+      } else {
+        // v: its neighbour label set minus the old / new label; a neighbour u: its set
+        // (plus v's old / new label) minus u's own label
+        const uint32_t hv = h.has_v ? 0xFFFFFFFFu : 0u;
+        const uint32_t ka = q == 0 ? ~(1u << a) : ~(1u << h.lx);
+        const uint32_t kd = q == 0 ? ~(1u << d) : ~(1u << h.lx);
+        wo = (uint32_t)__popc((h.bits | ((1u << a) & hv)) & ka);
+        wn = (uint32_t)__popc((h.bits | ((1u << d) & hv)) & kd);
+      }
+      wo = mine ? wo : 0u;
+      wn = mine ? wn : 0u;
+      // boundary changes if this flip is made (used only when it is accepted, which implies
+      // valid): 1/|B'| is read now, before the contiguity stages, so its L2 latency hides
+      // behind them
+      const uint64_t b_plus = ballot(go && mine && wo == 0 && wn > 0);
+      const uint64_t b_minus = ballot(go && mine && wo > 0 && wn == 0);
+      const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
+      const double invb_new = p.g.invb[bnodes + plus - minus];
       // ---- contiguity: 8-cell ring test, 7x7 window, exact race search when undecided
       const uint32_t rbits8 = rowbits(ballot(q >= 1 && q <= 8 && h.lx == a), row) >> 1;
       const int pN = rbits8 & 1, pW = (rbits8 >> 1) & 1, pE = (rbits8 >> 2) & 1, pS = (rbits8 >> 3) & 1;
@@ -1195,32 +1223,6 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         else if (!contig) n_conf += 1;
         retries = valid ? 0u : retries + 1u;
       }
-      // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
-      uint32_t wo = 0, wn = 0;
-      const bool mine = (q <= 4) & (h.x >= 0);
-      // branch-free (selects, no exec-mask if/else between v's lane and its neighbours')
-      if constexpr (MODE == FW_PROPOSE_CUTEDGE) {
-        const uint32_t wo_v = (uint32_t)(h.deg - m), wn_v = (uint32_t)(h.deg - nbd);
-        const uint32_t wo_u = h.cnt + (uint32_t)(h.has_v & (a != h.lx));
-        const uint32_t wn_u = h.cnt + (uint32_t)(h.has_v & (d != h.lx));
-        wo = q == 0 ? wo_v : wo_u;
-        wn = q == 0 ? wn_v : wn_u;
-      } else {
-        // v: its neighbour label set minus the old / new label; a neighbour u: its set
-        // (plus v's old / new label) minus u's own label
-        const uint32_t hv = h.has_v ? 0xFFFFFFFFu : 0u;
-        const uint32_t ka = q == 0 ? ~(1u << a) : ~(1u << h.lx);
-        const uint32_t kd = q == 0 ? ~(1u << d) : ~(1u << h.lx);
-        wo = (uint32_t)__popc((h.bits | ((1u << a) & hv)) & ka);
-        wn = (uint32_t)__popc((h.bits | ((1u << d) & hv)) & kd);
-      }
-      wo = mine ? wo : 0u;
-      wn = mine ? wn : 0u;
-      const uint64_t b_plus = ballot(valid && mine && wo == 0 && wn > 0);
-      const uint64_t b_minus = ballot(valid && mine && wo > 0 && wn == 0);
-      const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
-      // 1/|B'| (read now, used after the accept rule and commit)
-      const double invb_new = p.g.invb[bnodes + plus - minus];
       // ---- accept rule (lane dcut+D holds the tabulated bound; include/flipwalk.h)
       bool accepted;
       if (rule == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
