@@ -181,7 +181,8 @@ def main():
                          "line per shard; the N-GPU job's rate is total steps / max shard time: "
                          "scripts/shards.sh)")
     ap.add_argument("--ladder", default="interleaved", choices=["interleaved", "contiguous"],
-                    help="C5: base groups spread over the shards (default) or adjacent (round 1)")
+                    help="C5: base groups spread over the shards in snake order of the ladder octaves "
+                         "(default, workloads.ladder_base_index) or adjacent (round 1)")
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--base", type=float, default=None)
