@@ -162,6 +162,63 @@ def native_cpu_baseline(w, bounds, base, seed, seconds=10.0, workers=None):
     return out
 
 
+# ------------------------------------------------------------------ parity spot-check
+STAT_FIELDS = ("attempts", "steps", "accepts", "pop_fail", "contig_fail", "bfs_runs", "bfs_nodes",
+               "bfs_deg", "sum_deg", "acc_deg", "n_bchg", "yields", "sum_cut", "sum_bnodes",
+               "sum_invb", "cut", "bnodes", "npairs", "stuck")
+
+
+def check_ids(chains, n_check):
+    """Local chain indices to re-run on the oracle: both ends, the middle and an even spread."""
+    ids = {0, chains - 1, chains // 2, min(1, chains - 1)}
+    ids.update(int(x) for x in np.linspace(0, chains - 1, max(2, n_check)).round())
+    return sorted(ids)[:max(n_check, 4)]
+
+
+def parity_check(w, ch, bounds, base, seed, chain_id0, total_steps, n_check, workers):
+    """Checker leg (outside the timed region): re-run a spread of the benched chains on the C
+    oracle (oracle/flipchain_oracle.c) from the same initial plan for the same number of
+    counted steps, and compare the final plan, the populations and every stats field (the
+    fp64 sum bitwise) with what the GPU holds.  Trajectories do not depend on how the steps
+    were split into launches, so one oracle call covers warm-up plus timed launches."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from flipcomplexityempirical_amd.chain import PROPOSALS, metropolis_table
+    from oracle import oracle as O
+    ids = check_ids(ch.n_chains, n_check)
+    labs, st, pops = ch.labels(), ch.stats(), ch.pops()
+    mode = PROPOSALS[w.proposal] if isinstance(w.proposal, str) else int(w.proposal)
+    bases = np.broadcast_to(np.asarray(base, np.float64), (ch.n_chains,))
+    init = np.asarray(w.init, np.int16)
+
+    def one(i):
+        thr = metropolis_table(float(bases[i]), ch.dgraph.maxdeg)
+        lab0 = init if init.ndim == 1 else init[i]
+        olab, ost, opops, _ = O.run_chain(w.graph, lab0, w.k, mode, *bounds, thr, seed,
+                                          chain_id0 + i, total_steps)
+        bad = [f for f in STAT_FIELDS
+               if ost[f][0].tobytes() != np.asarray(st[f][i], ost[f].dtype).tobytes()]
+        if not np.array_equal(olab, labs[i]):
+            bad.append("labels")
+        if not np.array_equal(opops, pops[i]):
+            bad.append("pops")
+        return i, bad
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
+        res = list(ex.map(one, ids))
+    mism = {str(chain_id0 + i): bad for i, bad in res if bad}
+    return {"chains": len(ids), "equal": len(ids) - len(mism),
+            "global_ids": [chain_id0 + i for i in ids], "steps_per_chain": int(total_steps),
+            "compared": "final plan, populations, all 19 stats fields (sum_invb bitwise)",
+            "mismatches": mism, "oracle_s": round(time.perf_counter() - t0, 2)}
+
+
+def flipwalk_env():
+    """FLIPWALK_* overrides active in this process (they change launch plans, not trajectories)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("FLIPWALK_")}
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
@@ -191,6 +248,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check-chains", type=int, default=16,
+                    help="chains per rank re-run on the C oracle after the timed region and "
+                         "compared bit for bit (parity_check; 0 = off)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N>1 (nccl = RCCL over xGMI; gloo for rehearsals)")
     ap.add_argument("--same-device", action="store_true",
@@ -277,6 +337,26 @@ def main():
         steps_all, att_all, acc_all = float(steps_local), float(d["attempts"]), float(d["accepts"])
     hist_cut, hist_b = merge_histograms(ch.hist_cut(), ch.hist_b(), dist)
 
+    # checker leg, after the timed region: every rank re-runs a spread of its chains on the
+    # C oracle; the line carries the totals over ranks
+    pc = None
+    if args.check_chains > 0:
+        pc = parity_check(w, ch, bounds, base, args.seed, lo,
+                          (args.warmup + args.steps) * args.inner, args.check_chains,
+                          host_cores()[0])
+        yields_local = int(st1_arr["yields"].astype(np.uint64).sum())
+        if dist is not None:
+            t = torch.tensor([pc["chains"], pc["equal"], yields_local], dtype=torch.int64,
+                             device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            pc["chains"], pc["equal"], yields_all = (int(x) for x in t)
+            pc["ranks"] = world
+        else:
+            yields_all = yields_local
+        # every yield of every chain lands in exactly one bin of each merged histogram
+        pc["hist_yields_equal"] = bool(int(hist_cut.sum()) == yields_all ==
+                                       int(hist_b.sum()))
+
     kernel_ms = float(np.mean(kms))
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
@@ -339,7 +419,9 @@ def main():
                 "spatial_maps": bool(args.maps),
                 "flip_steps_per_chain_per_step": args.inner,
                 "parallelism": par,
+                "flipwalk_env": flipwalk_env(),
             },
+            "parity_check": pc,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

@@ -173,6 +173,10 @@ class Chains:
             thr_per = 1
         self.thr = np.ascontiguousarray(thr)
         self.seed, self.chain_id0 = int(seed), int(chain_id0)
+        # the configuration a checkpoint must carry besides the state (set_accept,
+        # set_schedule change it after creation)
+        self.accept_rule, self.node_flags = _lib.ACCEPT_CUT, None
+        self._sched, self._sched_t0 = None, 0
         h = _lib.ctypes.c_void_p()
         check(L.fw_chains_create(dgraph.handle, self.n_chains, self.k, ptr(lab), per_chain,
                                  self.mode, self.pop_lo, self.pop_hi, ptr(self.thr), thr_per,
@@ -228,6 +232,7 @@ class Chains:
         r = ACCEPT_RULES[rule] if isinstance(rule, str) else int(rule)
         fl = None if node_flags is None else np.ascontiguousarray(node_flags, np.uint8)
         check(_lib.load().fw_chains_set_accept(self._h, r, ptr(fl)))
+        self.accept_rule, self.node_flags = r, fl
 
     def set_schedule(self, rows=None, t0: int = 0) -> None:
         """Step-dependent bounds shared by every chain (fw_chains_set_schedule): a proposal
@@ -236,12 +241,13 @@ class Chains:
         it.  See ``schedule_rows``."""
         if rows is None:
             check(_lib.load().fw_chains_set_schedule(self._h, None, 0, 0))
+            self._sched, self._sched_t0 = None, 0
             return
         r = np.ascontiguousarray(rows, np.float64)
         if r.ndim != 2 or r.shape[1] != self.thr.shape[-1]:
             raise ValueError(f"schedule rows must be [n][{self.thr.shape[-1]}]")
-        self._sched = r
         check(_lib.load().fw_chains_set_schedule(self._h, ptr(r), r.shape[0], int(t0)))
+        self._sched, self._sched_t0 = r, int(t0)
 
     # ------------------------------------------------------------- district shapes
     def enable_ring(self, ring_u, ring_w) -> None:
@@ -270,7 +276,12 @@ class Chains:
         attempt counter: the counter-based RNG makes resume exact) and the histograms."""
         ck = {"labels": self.labels(), "stats": self.stats(), "hist_cut": self.hist_cut(),
               "hist_b": self.hist_b(), "seed": np.uint64(self.seed),
-              "chain_id0": np.int64(self.chain_id0), "thr": self.thr}
+              "chain_id0": np.int64(self.chain_id0), "thr": self.thr,
+              "mode": np.int32(self.mode), "accept_rule": np.int32(self.accept_rule)}
+        if self.node_flags is not None:
+            ck["node_flags"] = self.node_flags
+        if self._sched is not None:
+            ck["sched_rows"], ck["sched_t0"] = self._sched, np.int64(self._sched_t0)
         if getattr(self, "ring", None) is not None:
             ck["hist_ring"] = self.hist_ring()
             ck["ring_u"], ck["ring_w"] = self.ring
@@ -281,6 +292,9 @@ class Chains:
         ids): the chains continue exactly where the checkpointed ones stopped."""
         if int(ck["seed"]) != self.seed or int(ck["chain_id0"]) != self.chain_id0:
             raise ValueError("checkpoint of another seed / chain-id range")
+        if "mode" in ck and int(ck["mode"]) != self.mode:
+            raise ValueError(f"checkpoint of proposal mode {int(ck['mode'])}, handle has "
+                             f"{self.mode}")
         L = _lib.load()
         for what, key in ((_lib.READ_LABELS, "labels"), (_lib.READ_STATS, "stats"),
                           (_lib.READ_HIST_CUT, "hist_cut"), (_lib.READ_HIST_B, "hist_b")):
@@ -294,6 +308,14 @@ class Chains:
             self.enable_ring(ck["ring_u"], ck["ring_w"])
             a = np.ascontiguousarray(ck["hist_ring"], np.uint64)
             check(L.fw_chains_write(self._h, _lib.READ_HIST_RING, ptr(a), a.nbytes))
+        # the accept rule and the bound schedule the checkpointed chains ran under (after the
+        # plans: the boundary rule's flagged-node counts are taken from them)
+        if "accept_rule" in ck:
+            self.set_accept(int(ck["accept_rule"]), ck.get("node_flags"))
+        if "sched_rows" in ck:
+            self.set_schedule(ck["sched_rows"], int(ck["sched_t0"]))
+        elif "accept_rule" in ck:
+            self.set_schedule(None)
 
     def save_checkpoint(self, path: str) -> None:
         ck = self.checkpoint()
@@ -301,11 +323,14 @@ class Chains:
         np.savez(path, **ck)
 
     @classmethod
-    def from_checkpoint(cls, dgraph: "DeviceGraph", path: str, k: int, proposal="pairs",
+    def from_checkpoint(cls, dgraph: "DeviceGraph", path: str, k: int, proposal=None,
                         pop_bounds=None, percent: float = 0.05) -> "Chains":
-        """A new handle resumed from ``save_checkpoint`` output (numpy, no pickle)."""
+        """A new handle resumed from ``save_checkpoint`` output (numpy, no pickle), with the
+        proposal mode, accept rule and bound schedule the checkpointed chains ran under."""
         d = np.load(path, allow_pickle=False)
         labels = d["labels"]
+        if proposal is None:
+            proposal = int(d["mode"]) if "mode" in d.files else "pairs"
         ch = cls(dgraph, labels.shape[0], k, labels, proposal=proposal, pop_bounds=pop_bounds,
                  percent=percent, seed=int(d["seed"]), chain_id0=int(d["chain_id0"]),
                  thr=d["thr"])

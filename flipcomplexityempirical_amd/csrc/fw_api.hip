@@ -862,10 +862,20 @@ int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t byt
         pack_labels(lab + (size_t)i * n, n, c->lb, packed.data() + (size_t)i * c->p.lab_stride,
                     c->p.lab_stride);
       }
+      // the spatial maps carry per-node run state of the current plans (not part of a
+      // checkpoint): a new plan under them would resume with wrong maps, so refuse
+      if (c->d_acc)
+        return fail(FW_ESTATE, "plans cannot be written while the spatial maps are enabled");
       c->gcache_ok = false;  // group sums and counts are re-derived from the new plans
       HIPCHK(hipMemcpy(c->d_labels, packed.data(), packed.size(), hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(c->d_pops, pops.data(), sizeof(int64_t) * pops.size(),
                        hipMemcpyHostToDevice));
+      if (c->p.bcnt) {  // FW_ACCEPT_BOUNDARY's flagged-node counts follow the new plans
+        HIPCHK(hipMemset(c->d_bcnt, 0, sizeof(int32_t) * (size_t)c->n_chains * c->k));
+        if (fw_launch_bcnt_init(c->p, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+          return fail(FW_EHIP, "flag count re-init failed");
+      }
       return FW_OK;
     }
     case FW_READ_STATS:
@@ -874,6 +884,12 @@ int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t byt
       c->gcache_ok = false;  // cut / bnodes / npairs come from the caller's records
       HIPCHK(hipMemcpy(c->d_stats, host_src, need, hipMemcpyHostToDevice));
       c->ran = true;  // the initial state was yielded in the run being resumed
+      {  // the maps' 2^32 yield-index guard counts the yields already made
+        const fw_chain_stats* st = static_cast<const fw_chain_stats*>(host_src);
+        uint64_t ymax = 0;
+        for (int i = 0; i < c->n_chains; ++i) ymax = std::max<uint64_t>(ymax, st[i].yields);
+        c->max_yields = ymax;
+      }
       return FW_OK;
     case FW_READ_HIST_CUT:
       need = sizeof(uint64_t) * (c->g->nnz / 2 + 1);
@@ -1046,15 +1062,20 @@ int fw_chains_enable_ring(fw_chains* c, const int32_t* ring_u, const int32_t* ri
   }
   HIPCHK(hipSetDevice(g->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->d_ring) (void)hipFree(c->d_ring);
-  if (c->d_hist_ring) (void)hipFree(c->d_hist_ring);
-  c->d_ring = nullptr;
-  c->d_hist_ring = nullptr;
   if (!c->d_ring_node && hipMalloc(&c->d_ring_node, (size_t)g->n) != hipSuccess)
     return fail(FW_ENOMEM, "ring node flags");
-  if (hipMalloc(&c->d_ring, sizeof(int32_t) * 2 * (size_t)n_ring) != hipSuccess ||
-      hipMalloc(&c->d_hist_ring, sizeof(unsigned long long) * ring_bins(n_ring)) != hipSuccess)
+  // the new buffers first: on failure the handle keeps its previous ring intact
+  int32_t* d_ring = nullptr;
+  unsigned long long* d_hist = nullptr;
+  if (hipMalloc(&d_ring, sizeof(int32_t) * 2 * (size_t)n_ring) != hipSuccess ||
+      hipMalloc(&d_hist, sizeof(unsigned long long) * ring_bins(n_ring)) != hipSuccess) {
+    if (d_ring) (void)hipFree(d_ring);
     return fail(FW_ENOMEM, "ring histogram of %d edges", n_ring);
+  }
+  if (c->d_ring) (void)hipFree(c->d_ring);
+  if (c->d_hist_ring) (void)hipFree(c->d_hist_ring);
+  c->d_ring = d_ring;
+  c->d_hist_ring = d_hist;
   c->ring_u.assign(ring_u, ring_u + n_ring);
   c->ring_w.assign(ring_w, ring_w + n_ring);
   c->ring_n = n_ring;

@@ -214,8 +214,10 @@ int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes);
  * the district populations are recomputed from it), FW_READ_STATS (counters, sums and
  * the attempt counter; the stuck flag included), FW_READ_HIST_CUT, FW_READ_HIST_B or
  * FW_READ_HIST_RING.  A chain resumed from {labels, stats} continues exactly as the
- * uninterrupted chain (same proposals, same Metropolis draws).  The spatial maps and the
- * FW_ACCEPT_BOUNDARY counts are not part of a checkpoint. */
+ * uninterrupted chain (same proposals, same Metropolis draws).  The FW_ACCEPT_BOUNDARY
+ * flagged-node counts are recomputed from written plans; the spatial maps are not part of a
+ * checkpoint, and a plan write on a handle with maps enabled fails with FW_ESTATE.  A stats
+ * write also restores the yield count the maps' 2^32 index guard starts from. */
 int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t bytes);
 
 /* Zero the per-chain sums and the yield histograms (not the chain states). */

@@ -495,6 +495,54 @@ def test_checkpoint_resume_bit_exact(gpu_lib, name, path, monkeypatch, tmp_path)
     assert_stats_equal(ch2.stats(), ost)
 
 
+@pytest.mark.parametrize("name,rule,path", [("grid10_k2_bi", "boundary", "auto"),
+                                            ("grid30x18_k2_bi", "boundary", "wave64"),
+                                            ("grid12_k4_pairs", "bratio", "auto")])
+def test_checkpoint_carries_accept_rule(gpu_lib, name, rule, path, monkeypatch, tmp_path):
+    """A checkpoint taken under uniform_accept + boundary_condition (or the |B'|/|B| rule with
+    a bound schedule) resumes under the same rule in a new handle: the boundary rule's
+    flagged-node counts are rebuilt from the restored plans, and the resumed chains equal the
+    oracle's uninterrupted run.  A plan write under enabled spatial maps is refused."""
+    from flipcomplexityempirical_amd._lib import InvalidInitialState
+    from flipcomplexityempirical_amd.chain import annealing_table, schedule_rows
+    from flipcomplexityempirical_amd.graph import boundary_flags
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    g = case.graph
+    r = 1 if rule == "bratio" else 2
+    thr = annealing_table(0.1, 5, g.maxdeg) if rule == "bratio" else case.thr
+    flags = boundary_flags(g) if rule == "boundary" else None
+    sched = schedule_rows(0.1, _ramp, 40, 160, g.maxdeg) if rule == "bratio" else None
+    dg = DeviceGraph(g)
+    ch = Chains(dg, 8, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds, seed=13,
+                chain_id0=2, thr=thr)
+    ch.set_accept(rule, flags)
+    if sched:
+        ch.set_schedule(*sched)
+    ch.run(350)
+    path_ck = str(tmp_path / "ck.npz")
+    ch.save_checkpoint(path_ck)
+    ch2 = Chains.from_checkpoint(dg, path_ck, case.k, pop_bounds=case.bounds)
+    ch2.run(450)
+    labs, st = ch2.labels(), ch2.stats()
+    lo, hi = case.bounds
+    for i in range(8):
+        lab, ost = case.init.copy(), O.new_stats(1)
+        lab, ost, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, thr, 13, 2 + i, 800,
+                                     stats=ost, accept_rule=r, flags=flags, schedule=sched)
+        assert np.array_equal(labs[i], lab), (name, i)
+        assert_stats_equal(st[i:i + 1], ost)
+    ch3 = Chains(dg, 2, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds, seed=13)
+    ch3.enable_maps()
+    with pytest.raises(InvalidInitialState):
+        ch3.restore({k2: v[:2] if k2 in ("labels", "stats") else v
+                     for k2, v in ch.checkpoint().items()
+                     if k2 not in ("seed", "chain_id0")} | {"seed": 13, "chain_id0": 0})
+
+
 BIG_CASES = [  # (h, w, k, seed blocks or bands, proposal, base, env)
     ("big132_k8_pairs", 132, 132, 8, (2, 4), "pairs", 0.5, {"FLIPWALK_BIG_K8": "1"}),
     ("big132_k8_cut", 132, 132, 8, (2, 4), "cutedge", 1.5, {"FLIPWALK_BIG_K8": "1"}),
