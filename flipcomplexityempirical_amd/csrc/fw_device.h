@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fw_internal.h"
+#include "fw_math.h"
 
 // Explicit address spaces: every chain-state access must be a DS (LDS) or global
 // instruction.  Generic pointers let the compiler emit FLAT accesses, which are not
@@ -119,6 +120,17 @@ __device__ __forceinline__ uint32_t scale64(uint32_t x0, uint32_t x1, uint32_t P
 }
 __device__ __forceinline__ double u53(uint32_t x2, uint32_t x3) {
   return ((double)(x2 >> 5) * 67108864.0 + (double)(x3 >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// The sampled geometric wait of the state created by proposal attempt t of chain gid
+// (FW_WAIT_T0: the initial state), given lp = log1p(-|B|/(N^k - 1)) of that state: the
+// Philox block (t, hi(t) | 2^31, gid) of key seed, u = CPython random() of words (x0, x1),
+// wait = floor(log1p(-u) / lp) — the oracle's wait_draw (oracle/flipchain_oracle.c).
+__device__ __forceinline__ double wait_draw(uint64_t seed, uint64_t t, uint64_t gid, double lp) {
+  const U4 y = philox((uint32_t)t, (uint32_t)(t >> 32) | 0x80000000u, (uint32_t)gid,
+                      (uint32_t)(gid >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double lu = fw_log1p(-u53(y.x0, y.x1));
+  return lu == 0.0 ? 0.0 : floor(lu / lp);
 }
 
 // ---------------------------------------------------------------- packed labels
@@ -561,6 +573,18 @@ struct Ctx {
   int my_dr, my_dc;
 #ifdef FW_STAMPS
   uint32_t n_win = 0, n_bbs = 0, n_list = 0;  // contiguity checks by the path that decided
+  uint64_t c_win = 0, c_bbs = 0, c_list = 0;  // s_memtime cycles spent in each path
+  uint64_t n_bbl = 0;                          // bitboard levels run (decided or escaped)
+  __device__ static __forceinline__ uint64_t now() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+  }
+#define CTX_T0 const uint64_t t_c0_ = now(); uint64_t t_c1_ = t_c0_;
+#define CTX_LAP(field) do { const uint64_t t_ = now(); field += t_ - t_c1_; t_c1_ = t_; } while (0)
+#else
+#define CTX_T0
+#define CTX_LAP(field)
 #endif
 
   __device__ void init_roles() {
@@ -1103,6 +1127,7 @@ struct Ctx {
                                              uint64_t& bfs_deg) {
     if (m == 0) return false;
     if (m == 1) return true;
+    CTX_T0
     uint64_t cls = lane < m ? (1ull << lane) : 0ull;
     // source index (rank in am) of the source held by lane ln
     auto sx = [&](int ln) { return __popcll(am & ((1ull << ln) - 1ull)); };
@@ -1154,6 +1179,7 @@ struct Ctx {
 #ifdef FW_STAMPS
         n_win += 1;
 #endif
+        CTX_LAP(c_win);
         if (wv >= 0) return wv == 1;
       }
       if (bb) {  // bitboard search first; the list search past its window
@@ -1166,6 +1192,7 @@ struct Ctx {
 #ifdef FW_STAMPS
         n_bbs += 1;
 #endif
+        CTX_LAP(c_bbs);
         if (wv >= 0) {
           bfs_runs += 1;
           return wv == 1;
@@ -1190,10 +1217,13 @@ struct Ctx {
       const int val = rdl(h.x, Ls);
       if (lane == i) src = val;
     }
+    bool verdict;
     if constexpr (LB == 3 || LB == 5)
-      return race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
+      verdict = race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else
-      return race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);
+      verdict = race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);
+    if constexpr (GRID) CTX_LAP(c_list);
+    return verdict;
   }
 };
 

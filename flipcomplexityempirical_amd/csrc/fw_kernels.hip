@@ -136,6 +136,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     int64_t sum_cut = (int64_t)rfl64((uint64_t)stp->sum_cut);
     int64_t sum_bnodes = (int64_t)rfl64((uint64_t)stp->sum_bnodes);
     double sum_invb = stp->sum_invb;  // running total: keeps the oracle's summation order
+    // sampled geometric waits (FULL only): the running sum and the current state's draw
+    const bool waits_on = FULL && p.wsamp != nullptr;
+    double wsum = waits_on ? p.wsamp[2 * (size_t)c] : 0.0;
+    double wcur = waits_on ? p.wsamp[2 * (size_t)c + 1] : 0.0;
     // per-launch counters (added to the 64-bit totals at the end), held in VGPRs: the
     // chain's uniform state already fills the scalar file
     uint32_t n_steps = in_vgpr(0), n_acc = in_vgpr(0), n_popf = in_vgpr(0), n_conf = in_vgpr(0);
@@ -198,6 +202,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     auto observe = [&]() {
       n_yield += 1;
       rrun += 1;
+      if (waits_on) wsum += wcur;
       sum_cut += cut;
       sum_bnodes += bnodes;
       sum_invb += invb;
@@ -218,7 +223,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       hb += (lane == ib);
     };
-    if (yields0 == 0 && attempts == 0) observe();
+    if (yields0 == 0 && attempts == 0) {
+      if (waits_on) wcur = wait_draw(p.seed, FW_WAIT_T0, gid, p.wlp[bnodes]);
+      observe();
+    }
     // Philox batches on the VALU: lane l holds the draw of attempt (batch base + l); an
     // attempt reads its four words with v_readlane (no scalar round-key table to spill)
     U4 pb = {0u, 0u, 0u, 0u};
@@ -402,6 +410,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           if (lane == (int)a) bcnt -= 1;
           if (lane == (int)d) bcnt += 1;
         }
+        // the new state's wait draw (its proposal was attempt `attempts` - 1)
+        if (waits_on) wcur = wait_draw(p.seed, attempts - 1, gid, p.wlp[bnodes]);
         if (RN && p.ring_node[v]) {  // only a flip of a ring node can change the pair
           const int32_t np2 = ring_pair();
           if (np2 != rpair) {
@@ -428,6 +438,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       if (FULL && lane < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lane] = bcnt;
     }
     if (FULL && lane == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
+    if (waits_on && lane == 0) {
+      p.wsamp[2 * (size_t)c] = wsum;
+      p.wsamp[2 * (size_t)c + 1] = wcur;
+    }
     if (lane == 0) {
       stp->attempts = attempts;
       stp->steps += n_steps;
@@ -459,6 +473,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   CSTAMP_COUNT(8, C.n_win);
   CSTAMP_COUNT(9, C.n_bbs);
   CSTAMP_COUNT(10, C.n_list);
+  CSTAMP_COUNT(11, C.c_win);
+  CSTAMP_COUNT(12, C.c_bbs);
+  CSTAMP_COUNT(13, C.c_list);
 #endif
   CSTAMP_FLUSH
 }
@@ -718,7 +735,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
   if (p.use16) return fw_grid16_launch(p, grid, stream);
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
-                    p.ring_n > 0 || p.trace != nullptr;
+                    p.ring_n > 0 || p.trace != nullptr || p.wsamp != nullptr;
   void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0, full);
   // handles of different graphs share instantiations: set this handle's LDS size
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);

@@ -57,3 +57,8 @@ if cb[:6].sum():
         print(f"{nm:18s} {v / tot * 100:6.2f} %  {v / att:8.1f} clk/attempt")
     print(f"contiguity decided by: 7x7 window {cb[8] / att:.3f}/attempt, bitboard search "
           f"{cb[9] / att:.3f}, list search {cb[10] / att:.3f}")
+    if cb[11] + cb[12] + cb[13]:
+        print(f"contiguity cycles by path (per attempt / per run): 7x7 window "
+              f"{cb[11] / att:.0f} / {cb[11] / max(cb[8], 1):.0f}, bitboard {cb[12] / att:.0f} / "
+              f"{cb[12] / max(cb[9], 1):.0f}, list search {cb[13] / att:.0f} / "
+              f"{cb[13] / max(cb[10], 1):.0f}")

@@ -151,3 +151,48 @@ def test_run_sharded_two_ranks_slices_per_chain_inputs(tmp_path):
                         base=bases, seed=SEED)
     assert np.array_equal(got["hc"], ref.hist_cut) and np.array_equal(got["hb"], ref.hist_b)
     assert np.array_equal(got["st"], ref.stats.view(np.uint8))
+
+
+def _gpu_sharded_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from test_distributed import _sharded_inputs
+    from flipcomplexityempirical_amd.distributed import run_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g, init, bases, bounds = _sharded_inputs()
+    # the real engine (chain.run_chains -> libflipwalk.so), every rank on device 0
+    res, hc, hb, st = run_sharded(g, init, 4, N_TOTAL, STEPS, dist, device=0,
+                                  proposal="pairs", pop_bounds=bounds, base=bases, seed=SEED)
+    lo, hi = shard_range(N_TOTAL, world, rank)
+    assert len(res.stats) == hi - lo
+    np.savez(out + f".{rank}.npz", labels=res.labels)
+    if rank == 0:
+        np.savez(out, hc=hc, hb=hb, st=st.view(np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_run_sharded_two_ranks_bit_identical(tmp_path, gpu_lib):
+    """run_sharded with the GPU engine in 2 gloo ranks (both on device 0): each rank's
+    handle runs its id range with its rows of the per-chain plans and bases; the merged
+    histograms and stats equal ONE handle running all chains, and the oracle, bit for bit."""
+    from flipcomplexityempirical_amd.chain import run_chains
+    out = str(tmp_path / "gpu_sharded.npz")
+    mp.start_processes(_gpu_sharded_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    g, init, bases, bounds = _sharded_inputs()
+    one = run_chains(g, init, 4, N_TOTAL, STEPS, proposal="pairs", pop_bounds=bounds, base=bases,
+                     seed=SEED)
+    assert np.array_equal(got["hc"], one.hist_cut) and np.array_equal(got["hb"], one.hist_b)
+    assert np.array_equal(got["st"], one.stats.view(np.uint8))
+    labs = np.concatenate([np.load(out + f".{r}.npz")["labels"] for r in range(2)])
+    assert np.array_equal(labs, one.labels)
+    ref = oracle_engine(g, init, 4, N_TOTAL, STEPS, proposal="pairs", pop_bounds=bounds,
+                        base=bases, seed=SEED)
+    assert np.array_equal(one.hist_cut, ref.hist_cut) and np.array_equal(one.hist_b, ref.hist_b)
+    assert np.array_equal(one.stats.view(np.uint8), ref.stats.view(np.uint8))
