@@ -18,7 +18,7 @@ FW_OK = 0
 FW_EINVAL, FW_EHIP, FW_ESTATE, FW_EUNSUPPORTED, FW_ENOMEM = -1, -2, -3, -4, -5
 PROPOSE_BI, PROPOSE_PAIRS, PROPOSE_CUTEDGE = 0, 1, 2
 READ_LABELS, READ_STATS, READ_HIST_CUT, READ_HIST_B, READ_POPS = 0, 1, 2, 3, 4
-READ_HIST_RING, READ_RING_PAIR = 5, 6
+READ_HIST_RING, READ_RING_PAIR, READ_WAITS = 5, 6, 7
 MAP_CUT_TIMES, MAP_NUM_FLIPS, MAP_PART_SUM, MAP_LAST_FLIPPED = 0, 1, 2, 3
 MAP_SUM, MAP_FINALIZE = 1, 2
 ACCEPT_CUT, ACCEPT_BRATIO, ACCEPT_BOUNDARY = 0, 1, 2
@@ -72,6 +72,7 @@ SIGNATURES = [
     ("fw_chains_set_schedule", ctypes.c_int, [_P, _P, _I32, _I64]),
     ("fw_chains_enable_maps", ctypes.c_int, [_P, _P]),
     ("fw_chains_enable_ring", ctypes.c_int, [_P, _P, _P, _I32]),
+    ("fw_chains_enable_waits", ctypes.c_int, [_P, _P]),
     ("fw_chains_read_map", ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, ctypes.c_size_t]),
     ("fw_eval_flips", ctypes.c_int,
      [_P, _P, _I32, _P, _P, _I32, _I64, _I64, _P, _P, _P, _P]),

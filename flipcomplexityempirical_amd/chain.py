@@ -92,11 +92,19 @@ def expected_wait_sum(stats, n_nodes: int, k: int) -> np.ndarray:
     return M * stats["sum_invb"] - stats["yields"].astype(np.float64)
 
 
+def wait_prob_table(n_nodes: int, k: int) -> np.ndarray:
+    """p_b = len(b_nodes) / (N**k - 1) for every boundary size b = 0..N, divided as
+    geom_wait divides (grid_chain_sec11.py:148: Python int / int, correctly rounded)."""
+    M = int(n_nodes) ** int(k) - 1
+    return np.array([b / M for b in range(int(n_nodes) + 1)], np.float64)
+
+
 def write_wait_txt(path: str, wait_sum: float) -> None:
     """The reference's only text output (grid_chain_sec11.py:410-411):
-    ``wfile.write(str(sum(waits)))``.  ``wait_sum`` here is the Rao-Blackwellised
-    expectation of the geom_wait sum (expected_wait_sum), written as the nearest integer
-    like the reference's sum of integer draws."""
+    ``wfile.write(str(sum(waits)))``.  ``wait_sum`` is either the sampled sum
+    (``Chains.sampled_waits``, the reference's own kind of value: a sum of integer draws)
+    or the Rao-Blackwellised expectation (expected_wait_sum), written as the nearest
+    integer."""
     with open(path, "w") as f:
         f.write(str(int(round(float(wait_sum)))))
 
@@ -177,6 +185,7 @@ class Chains:
         # set_schedule change it after creation)
         self.accept_rule, self.node_flags = _lib.ACCEPT_CUT, None
         self._sched, self._sched_t0 = None, 0
+        self.waits_on = False
         h = _lib.ctypes.c_void_p()
         check(L.fw_chains_create(dgraph.handle, self.n_chains, self.k, ptr(lab), per_chain,
                                  self.mode, self.pop_lo, self.pop_hi, ptr(self.thr), thr_per,
@@ -249,6 +258,24 @@ class Chains:
         check(_lib.load().fw_chains_set_schedule(self._h, ptr(r), r.shape[0], int(t0)))
         self._sched, self._sched_t0 = r, int(t0)
 
+    # ------------------------------------------------------------- sampled waits
+    def enable_sampled_waits(self) -> None:
+        """Draw geom_wait per state object (grid_chain_sec11.py:147-148, cached and re-used
+        on re-yield) and sum it over yields (:368, :410-411); see fw_chains_enable_waits.
+        Call before the first run."""
+        pt = np.ascontiguousarray(wait_prob_table(self.dgraph.n, self.k))
+        check(_lib.load().fw_chains_enable_waits(self._h, ptr(pt)))
+        self.waits_on = True
+
+    def waits(self) -> np.ndarray:
+        """float64 [n_chains, 2]: {sum of the sampled waits over yields, the current
+        state's draw}."""
+        return self._read(_lib.READ_WAITS, np.empty((self.n_chains, 2), np.float64))
+
+    def sampled_waits(self) -> np.ndarray:
+        """Per chain, sum(waits) of grid_chain_sec11.py:410 (integer-valued floats)."""
+        return self.waits()[:, 0].copy()
+
     # ------------------------------------------------------------- district shapes
     def enable_ring(self, ring_u, ring_w) -> None:
         """Count yields per pair of first two cut ring edges (boundary_slope and the
@@ -282,6 +309,8 @@ class Chains:
             ck["node_flags"] = self.node_flags
         if self._sched is not None:
             ck["sched_rows"], ck["sched_t0"] = self._sched, np.int64(self._sched_t0)
+        if self.waits_on:
+            ck["waits"] = self.waits()
         if getattr(self, "ring", None) is not None:
             ck["hist_ring"] = self.hist_ring()
             ck["ring_u"], ck["ring_w"] = self.ring
@@ -296,6 +325,8 @@ class Chains:
             raise ValueError(f"checkpoint of proposal mode {int(ck['mode'])}, handle has "
                              f"{self.mode}")
         L = _lib.load()
+        if "waits" in ck and not self.waits_on:
+            self.enable_sampled_waits()
         for what, key in ((_lib.READ_LABELS, "labels"), (_lib.READ_STATS, "stats"),
                           (_lib.READ_HIST_CUT, "hist_cut"), (_lib.READ_HIST_B, "hist_b")):
             a = np.ascontiguousarray(ck[key])
@@ -304,6 +335,9 @@ class Chains:
                 if a.shape != (self.n_chains,):
                     raise ValueError("checkpoint of another chain count")
             check(L.fw_chains_write(self._h, what, ptr(a), a.nbytes))
+        if "waits" in ck:
+            a = np.ascontiguousarray(ck["waits"], np.float64)
+            check(L.fw_chains_write(self._h, _lib.READ_WAITS, ptr(a), a.nbytes))
         if "hist_ring" in ck:
             self.enable_ring(ck["ring_u"], ck["ring_w"])
             a = np.ascontiguousarray(ck["hist_ring"], np.uint64)

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "fw_internal.h"
+#include "fw_math.h"
 
 namespace {
 
@@ -169,6 +170,8 @@ struct fw_chains {
   // fw_chains_enable_ring
   int32_t ring_n = 0;
   std::vector<int32_t> ring_u, ring_w;
+  double* d_wsamp = nullptr;  // fw_chains_enable_waits: [n_chains][2] {sum, current draw}
+  double* d_wlp = nullptr;    // [n+1] log1p(-p_b)
   int32_t* d_ring = nullptr;              // [2][ring_n] endpoints
   uint8_t* d_ring_node = nullptr;         // [n]
   unsigned long long* d_hist_ring = nullptr;  // [ring_n^2 + 1]
@@ -279,7 +282,7 @@ extern "C" {
 
 const char* fw_last_error(void) { return g_err.c_str(); }
 
-int32_t fw_version(void) { return 0x000400; }
+int32_t fw_version(void) { return 0x000500; }
 
 int32_t fw_device_count(void) {
   int c = 0;
@@ -448,7 +451,8 @@ void fw_chains_destroy(fw_chains* c) {
   void* bufs[] = {c->d_labels, c->d_stats, c->d_pops, c->d_thr, c->d_thr53, c->d_hist_cut, c->d_hist_b,
                   c->d_spill,  c->d_next,  c->d_acc,  c->d_nf,   c->d_lf,       c->d_ps,
                   c->d_pend,   c->d_labval, c->d_flags, c->d_bcnt, c->d_sched, c->d_sched53,
-                  c->d_ring,   c->d_ring_node, c->d_hist_ring, c->d_gscr, c->d_segdone};
+                  c->d_ring,   c->d_ring_node, c->d_hist_ring, c->d_gscr, c->d_segdone,
+                  c->d_wsamp,  c->d_wlp};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -836,6 +840,12 @@ int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes) {
       }
       return FW_OK;
     }
+    case FW_READ_WAITS:
+      if (!c->d_wsamp) return fail(FW_ESTATE, "sampled waits are not enabled");
+      need = sizeof(double) * 2 * (size_t)c->n_chains;
+      if (bytes < need) return fail(FW_EINVAL, "waits need %zu bytes", need);
+      HIPCHK(hipMemcpy(host_dst, c->d_wsamp, need, hipMemcpyDeviceToHost));
+      return FW_OK;
     default:
       return fail(FW_EINVAL, "unknown read kind %d", what);
   }
@@ -906,6 +916,12 @@ int fw_chains_write(fw_chains* c, int32_t what, const void* host_src, size_t byt
       need = sizeof(uint64_t) * ring_bins(c->ring_n);
       if (bytes < need) return fail(FW_EINVAL, "hist_ring needs %zu bytes", need);
       HIPCHK(hipMemcpy(c->d_hist_ring, host_src, need, hipMemcpyHostToDevice));
+      return FW_OK;
+    case FW_READ_WAITS:
+      if (!c->d_wsamp) return fail(FW_ESTATE, "sampled waits are not enabled");
+      need = sizeof(double) * 2 * (size_t)c->n_chains;
+      if (bytes < need) return fail(FW_EINVAL, "waits need %zu bytes", need);
+      HIPCHK(hipMemcpy(c->d_wsamp, host_src, need, hipMemcpyHostToDevice));
       return FW_OK;
     default:
       return fail(FW_EINVAL, "fw_chains_write: unsupported kind %d", what);
@@ -1044,6 +1060,33 @@ int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values) {
   const int le = fw_launch_map_init(p, c->stream);
   if (le != 0) return fail(FW_EHIP, "map init launch failed: %s", hipGetErrorString((hipError_t)le));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return FW_OK;
+}
+
+int fw_chains_enable_waits(fw_chains* c, const double* p_table) {
+  if (!c || !p_table) return fail(FW_EINVAL, "fw_chains_enable_waits: null");
+  if (c->ran) return fail(FW_ESTATE, "enable the sampled waits before the first run");
+  const int n = c->g->n;
+  std::vector<double> lp((size_t)n + 1);
+  for (int b = 0; b <= n; ++b) {
+    if (!(p_table[b] >= 0.0 && p_table[b] < 1.0))
+      return fail(FW_EINVAL, "p_table[%d] = %g outside [0, 1)", b, p_table[b]);
+    lp[b] = fw_log1p(-p_table[b]);
+  }
+  HIPCHK(hipSetDevice(c->g->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (!c->d_wsamp) {
+    if (hipMalloc(&c->d_wsamp, sizeof(double) * 2 * (size_t)c->n_chains) != hipSuccess ||
+        hipMalloc(&c->d_wlp, sizeof(double) * lp.size()) != hipSuccess) {
+      if (c->d_wsamp) (void)hipFree(c->d_wsamp);
+      c->d_wsamp = nullptr;
+      return fail(FW_ENOMEM, "sampled-wait buffers");
+    }
+  }
+  HIPCHK(hipMemcpy(c->d_wlp, lp.data(), sizeof(double) * lp.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(c->d_wsamp, 0, sizeof(double) * 2 * (size_t)c->n_chains));
+  c->p.wsamp = c->d_wsamp;
+  c->p.wlp = c->d_wlp;
   return FW_OK;
 }
 

@@ -710,6 +710,10 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     int32_t stuck = has ? stp->stuck : 1;
     int64_t sum_cut = stp->sum_cut, sum_bnodes = stp->sum_bnodes;
     double sum_invb = stp->sum_invb;
+    // sampled geometric waits (FULL only): the running sum and the current state's draw
+    const bool waits_on = FULL && p.wsamp != nullptr;
+    double wsum = waits_on ? p.wsamp[2 * (size_t)cc] : 0.0;
+    double wcur = waits_on ? p.wsamp[2 * (size_t)cc + 1] : 0.0;
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0, n_sdeg = 0, n_adeg = 0, n_bchg = 0;
     uint32_t retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
@@ -803,6 +807,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     auto observe = [&](bool on) {
       if (!on) return;
       if (FULL) rrun += 1;
+      if (waits_on) wsum += wcur;
       sum_cut += cut;
       sum_bnodes += bnodes;
       sum_invb += invb;
@@ -827,6 +832,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       hb0 += ib == q;
       hb1 += ib == q + ROW;
     };
+    if (waits_on && first) wcur = wait_draw(p.seed, FW_WAIT_T0, gid, p.wlp[bnodes]);
     observe(first);
 
     // Philox batches: lane q of a row holds the draw of its chain's attempt (base + q).
@@ -1300,6 +1306,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
           if ((uint32_t)q == a) bcnt -= 1;
           if ((uint32_t)q == d) bcnt += 1;
         }
+        // the new state's wait draw (its proposal was attempt att0 + n_att - 1)
+        if (waits_on) wcur = wait_draw(p.seed, att0 + (uint64_t)(n_att - 1u), gid, p.wlp[bnodes]);
       }
       observe(valid);
       STAMP(5);  // counters, observe
@@ -1319,6 +1327,10 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       if (q < k) p.pops[(size_t)c * k + q] = (int64_t)pops;
       if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
       if (q == 0 && maps_on) pend_store(p, c, pend);
+      if (q == 0 && waits_on) {
+        p.wsamp[2 * (size_t)c] = wsum;
+        p.wsamp[2 * (size_t)c + 1] = wcur;
+      }
       // the 136-byte stats record as 16-byte read-modify-writes by row-lanes 0..8 (every
       // lane of a row holds the row-uniform values): 9 requests instead of 19 4- and 8-byte
       // ones (no measurable change in time or PMC WRITE_SIZE: profiles/r02/c3)
@@ -1443,7 +1455,8 @@ int fw_grid16_lb(int G, int k) { return k <= 4 ? 2 : (is_big(G) ? 3 : 4); }
 
 void* fw_grid16_fn(const FwRunParams& p) {
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
-                    p.ring_n > 0 || p.trace != nullptr || p.g.pop != nullptr;
+                    p.ring_n > 0 || p.trace != nullptr || p.g.pop != nullptr ||
+                    p.wsamp != nullptr;
   return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
 }
 

@@ -111,6 +111,10 @@ struct FwRunParams {
   const int32_t* ring_w;
   const uint8_t* ring_node;
   unsigned long long* hist_ring;  // [ring_n^2 + 1]
+  // sampled geometric waits (fw_chains_enable_waits; nullptr: off): per chain {sum over
+  // yields, the current state's draw}; wlp [n+1] = log1p(-b / (N^k - 1)) (fw_math.h)
+  double* wsamp;
+  const double* wlp;
 };
 
 // fw_chains_read_map: finalise maps of a chain range (see include/flipwalk.h)

@@ -88,6 +88,8 @@ extern "C" {
 #define FW_READ_POPS 4     /* int64  [n_chains][k] district populations       */
 #define FW_READ_HIST_RING 5 /* uint64 [n_ring*n_ring+1] yields per ring pair (below) */
 #define FW_READ_RING_PAIR 6 /* int32  [n_chains][2] current ring pair (i, j), -1 = none */
+#define FW_READ_WAITS 7    /* double [n_chains][2] {sum of sampled waits over yields, the
+                              current state's draw} (fw_chains_enable_waits)             */
 
 /* ---- district-shape observable (fw_chains_enable_ring) ----------------------
  * boundary_slope (grid_chain_sec11.py:55-78; Frankenstein_chain.py:57-80) collects the
@@ -148,8 +150,8 @@ typedef struct fw_chains fw_chains;
 /* Thread-local description of the last error on this thread. */
 const char* fw_last_error(void);
 
-/* Library/ABI version, e.g. 0x000400 for 0.4.0 (0.2: spatial maps; 0.3: bound
- * schedules; 0.4: ring observable, checkpoint/resume). */
+/* Library/ABI version, e.g. 0x000500 for 0.5.0 (0.2: spatial maps; 0.3: bound
+ * schedules; 0.4: ring observable, checkpoint/resume; 0.5: sampled geometric waits). */
 int32_t fw_version(void);
 
 /* Number of visible HIP devices (0 when none; never fails). */
@@ -249,6 +251,19 @@ int fw_chains_enable_maps(fw_chains* c, const int64_t* label_values);
  * picks "the first two".  Zeroes the ring histogram; may be called between runs. */
 int fw_chains_enable_ring(fw_chains* c, const int32_t* ring_u, const int32_t* ring_w,
                           int32_t n_ring);
+
+/* Turn on sampled geometric waits for every chain (before the first run): geom_wait
+ * (grid_chain_sec11.py:147-148) = int(np.random.geometric(len(b_nodes)/(N**k - 1))) - 1,
+ * drawn once per state object and re-used when a Metropolis rejection re-yields it
+ * (:368; the Partition caches it), summed over yields (:410-411).  p_table [n+1] holds
+ * b/(N^k - 1) for every boundary size b, divided as the reference divides (Python int /
+ * int).  The state created by proposal attempt t of global chain g (the initial state:
+ * t = 2^63 - 1) draws the Philox block key = seed, ctr = (lo32(t), hi32(t) | 2^31,
+ * lo32(g), hi32(g)), takes u = CPython random() of its words (x0, x1) and waits
+ * floor(log1p(-u) / log1p(-p)) (inversion; log1p evaluated in plain IEEE double
+ * operations, so every implementation agrees bit for bit).  Read / write with
+ * FW_READ_WAITS.  The Rao-Blackwellised expectation (stats sum_invb) stays available. */
+int fw_chains_enable_waits(fw_chains* c, const double* p_table);
 
 /* Read a map (FW_MAP_*) of chains [chain0, chain0 + n_chains) as int64
  * [n_chains][len], or with FW_MAP_SUM its sum over those chains [len]; len is

@@ -94,6 +94,24 @@ typedef struct {
   const int64_t* pop; /* NULL = all ones */
 } graph_t;
 
+/* Sampled geometric waits (geom_wait, grid_chain_sec11.py:147-148, read per yield at :368,
+ * summed and written at :410-411): int(np.random.geometric(len(b_nodes)/(N**k - 1))) - 1,
+ * drawn ONCE per state object and re-used when a Metropolis rejection re-yields it (the
+ * Partition caches updater values).  Restated as one inversion draw per state: the state
+ * created by proposal attempt t of chain g (the initial state: t = 2^63 - 1) draws the
+ * Philox block key = seed, ctr = (lo32(t), hi32(t) | 2^31, lo32(g), hi32(g)) and takes
+ * u = CPython random() of its words (x0, x1); then wait = floor(log1p(-u) / lp[|B|]) with
+ * lp[b] = log1p(-b/(N^k - 1)) (the geometric's number of failures, P(wait >= w) =
+ * (1-p)^w).  log1p is orc_log1p below, operation for operation the kernels' fw_log1p
+ * (flipcomplexityempirical_amd/csrc/fw_math.h), so the draws are bit-identical.  For
+ * p below 2^-52 (k >= 5 on large graphs) the reference's int64 draw overflows; this
+ * fp64 inversion does not (the value is then ~ -log(1-u)/p). */
+typedef struct orc_waits {
+  const double* lp; /* [n+1] log1p(-p_b), p_b = b/(N^k - 1) as the reference divides */
+  double sum;       /* sum over yields of the current state's draw */
+  double cur;       /* the current state's draw */
+} orc_waits;
+
 typedef struct {
   graph_t g;
   int32_t k, mode;
@@ -118,7 +136,57 @@ typedef struct {
   int64_t sched_t0;
   const uint8_t* flags;  /* [n] boundary_node flags (FW_ACCEPT_BOUNDARY), may be NULL */
   int64_t* bcnt;         /* [k] flagged nodes per district */
+  orc_waits* waits;      /* sampled geometric waits, may be NULL */
 } chain_t;
+
+/* log1p for -1 < x <= 0 by the classic reduction 1 + x = 2^k m, m in [sqrt(2)/2, sqrt(2)),
+ * log m = 2 atanh(f / (2 + f)) (f = m - 1) by a degree-14 odd series, plus the rounding
+ * correction of 1 + x; every operation IEEE double, no fused multiply-add. */
+double orc_log1p(double x) {
+  if (x == 0.0) return x;
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01;
+  const double Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01;
+  const double Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01;
+  const double Lg7 = 1.479819860511658591e-01;
+  const double u = 1.0 + x;
+  uint64_t bits;
+  memcpy(&bits, &u, 8);
+  int k = (int)((bits >> 52) & 0x7FF) - 1023;
+  uint64_t mb = (bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+  if (mb > 0x3FF6A09E667F3BCCull) { /* m >= sqrt(2): halve it */
+    mb -= 0x0010000000000000ull;
+    k += 1;
+  }
+  double m;
+  memcpy(&m, &mb, 8);
+  double c = k > 0 ? 1.0 - (u - x) : x - (u - 1.0);
+  c = c / u;
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+}
+
+#define ORC_WAIT_T0 0x7FFFFFFFFFFFFFFFull /* attempt index of the initial state's draw */
+
+/* the sampled wait of the state created by attempt t (|B| = b) */
+static double wait_draw(const chain_t* c, uint64_t t, int32_t b) {
+  uint32_t ctr[4] = {(uint32_t)t, (uint32_t)(t >> 32) | 0x80000000u, (uint32_t)c->chain,
+                     (uint32_t)(c->chain >> 32)};
+  uint32_t key[2] = {(uint32_t)c->seed, (uint32_t)(c->seed >> 32)};
+  uint32_t x[4];
+  orc_philox4x32_10(ctr, key, x);
+  const double lu = orc_log1p(-orc_u53(x[0], x[1]));
+  const double lp = c->waits->lp[b];
+  return lu == 0.0 ? 0.0 : floor(lu / lp);
+}
 
 /* The reference driver's spatial observables, updated once per yield exactly as
  * grid_chain_sec11.py:383-384 and :396-400 do (Frankenstein_chain.py:413-425 and
@@ -505,6 +573,7 @@ static void ring_yield(chain_t* c) {
 }
 
 static void yield_obs(chain_t* c) {
+  if (c->waits) c->waits->sum += c->waits->cur;
   if (c->maps) maps_yield(c);
   if (c->ring) ring_yield(c);
   c->st.yields++;
@@ -604,7 +673,7 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
                      uint64_t* hist_cut, uint64_t* hist_b, int32_t* trace, int64_t* pops_out,
                      orc_maps* maps, int32_t accept_rule, const uint8_t* flags,
                      const double* sched, int32_t sched_rows, int64_t sched_t0,
-                     const orc_ring* ring) {
+                     const orc_ring* ring, orc_waits* waits) {
   chain_t c;
   if (setup(&c, rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr)) {
     teardown(&c);
@@ -623,8 +692,12 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
   c.sched = sched_rows > 0 ? sched : NULL;
   c.sched_rows = sched_rows;
   c.sched_t0 = sched_t0;
+  c.waits = waits;
   derive(&c);
-    if (c.st.yields == 0 && c.st.attempts == 0) yield_obs(&c);
+  if (c.st.yields == 0 && c.st.attempts == 0) {
+    if (waits) waits->cur = wait_draw(&c, ORC_WAIT_T0, c.st.bnodes);
+    yield_obs(&c);
+  }
   for (int64_t s = 0; s < steps && !c.st.stuck; ++s) {
     int32_t retries = 0;
     int32_t v = -1, dcut = 0;
@@ -672,6 +745,7 @@ int orc_run_chain_ex(const int32_t* rowptr, const int32_t* col, const int64_t* p
       c.st.acc_deg += (uint64_t)(rowptr[v + 1] - rowptr[v]);
       c.st.n_bchg += (uint64_t)commit(&c, v, b, dcut);
       if (maps) maps->cur_f = v;
+      if (waits) waits->cur = wait_draw(&c, c.st.attempts - 1, c.st.bnodes);
     }
     if (trace) trace[s] = accepted ? v : -1;
     yield_obs(&c);
@@ -690,7 +764,7 @@ int orc_run_chain(const int32_t* rowptr, const int32_t* col, const int64_t* pop,
                   uint64_t* hist_b, int32_t* trace, int64_t* pops_out) {
   return orc_run_chain_ex(rowptr, col, pop, n, grid_w, k, mode, pop_lo, pop_hi, thr, seed,
                           chain_id, labels, stats, steps, max_retries, hist_cut, hist_b, trace,
-                          pops_out, NULL, FW_ACCEPT_CUT, NULL, NULL, 0, 0, NULL);
+                          pops_out, NULL, FW_ACCEPT_CUT, NULL, NULL, 0, 0, NULL, NULL);
 }
 
 /* Per-flip evaluation on one state (the fw_eval_flips contract). */

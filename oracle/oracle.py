@@ -66,7 +66,9 @@ def lib():
         ]
         L.orc_run_chain.restype = ctypes.c_int
         L.orc_run_chain_ex.argtypes = L.orc_run_chain.argtypes + [
-            _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int64, _P]
+            _P, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_int64, _P, _P]
+        L.orc_log1p.argtypes = [ctypes.c_double]
+        L.orc_log1p.restype = ctypes.c_double
         L.orc_run_chain_ex.restype = ctypes.c_int
         L.orc_eval_flips.argtypes = [
             _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
@@ -147,9 +149,35 @@ class Ring:
         self._s = _OrcRing(_ptr(self.u), _ptr(self.w), n, 0, _ptr(self.hist))
 
 
+class _OrcWaits(ctypes.Structure):
+    _fields_ = [("lp", _P), ("sum", ctypes.c_double), ("cur", ctypes.c_double)]
+
+
+def log1p(x):
+    return lib().orc_log1p(float(x))
+
+
+class Waits:
+    """Sampled geometric waits of one chain (geom_wait, grid_chain_sec11.py:147-148): one
+    inversion draw per state object, re-used on re-yield; ``p_table`` [n+1] holds
+    b / (N**k - 1) as the reference divides (chain.wait_prob_table)."""
+
+    def __init__(self, p_table):
+        self.lp = np.array([log1p(-float(p)) for p in p_table], np.float64)
+        self._s = _OrcWaits(_ptr(self.lp), 0.0, 0.0)
+
+    @property
+    def sum(self):
+        return self._s.sum
+
+    @property
+    def cur(self):
+        return self._s.cur
+
+
 def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps,
               max_retries=1 << 20, stats=None, hist_cut=None, hist_b=None, trace=False,
-              maps=None, accept_rule=0, flags=None, schedule=None, ring=None):
+              maps=None, accept_rule=0, flags=None, schedule=None, ring=None, waits=None):
     """Run one chain on the CPU oracle.  ``graph`` needs rowptr/col/pop/n/grid_w.
 
     Returns (labels, stats, pops, trace-or-None); ``labels`` is a new int16 array.
@@ -157,7 +185,8 @@ def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps
     ``accept_rule`` is FW_ACCEPT_* (0 cut_accept, 1 the |B'|/|B| rule, 2 uniform_accept
     with boundary_condition over the uint8 ``flags``).  ``schedule`` = (rows, t0): the
     step-dependent bounds of fw_chains_set_schedule; ``ring`` (an oracle ``Ring``)
-    accumulates the district-shape observable.
+    accumulates the district-shape observable; ``waits`` (an oracle ``Waits``) the sampled
+    geometric waits (its ``sum`` / ``cur`` carry over between calls, like ``stats``).
     """
     srows, st0 = (None, 0) if schedule is None else schedule
     if srows is not None:
@@ -175,6 +204,7 @@ def run_chain(graph, labels, k, mode, pop_lo, pop_hi, thr, seed, chain_id, steps
         None if maps is None else ctypes.byref(maps._s), int(accept_rule), _ptr(fl),
         _ptr(srows), 0 if srows is None else int(srows.shape[0]), int(st0),
         None if ring is None else ctypes.byref(ring._s),
+        None if waits is None else ctypes.byref(waits._s),
     )
     if rc != 0:
         raise MemoryError("oracle allocation failed")

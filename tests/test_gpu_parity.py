@@ -640,3 +640,71 @@ def test_big_grid_full_instantiation(gpu_lib, feature, monkeypatch):
             assert np.array_equal(ch.read_map("num_flips", (i, i + 1))[0], maps.num_flips)
     if feature == "ring":
         assert np.array_equal(ch.hist_ring(), ring.hist)
+
+
+WAIT_CASES = [("grid10_k2_bi", "auto"), ("grid12_k4_pairs", "auto"), ("grid20_k4_mu", "wave64"),
+              ("grid16x24_k8", "auto"), ("sec11_a2_k2", "auto"), ("tract_k4", "auto"),
+              ("frank_a2_k2", "auto"), ("grid12_k4_cut", "wave64")]
+
+
+@pytest.mark.parametrize("name,path", WAIT_CASES, ids=[f"{p}-{n}" for n, p in WAIT_CASES])
+def test_sampled_waits_bit_exact(gpu_lib, name, path, monkeypatch, tmp_path):
+    """Sampled geom_wait (grid_chain_sec11.py:147-148: one geometric draw per state object,
+    re-used on re-yield, summed over yields): the kernels' per-chain {sum, current draw}
+    equal the oracle's bit for bit across launches and across a checkpoint / resume (the
+    shared fw_log1p / orc_log1p operation sequence), on both kernels."""
+    from flipcomplexityempirical_amd.chain import wait_prob_table
+    if path == "wave64":
+        monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    else:
+        monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    case = {c.name: c for c in CASES}[name]
+    g = case.graph
+    n_chains, seed, id0, steps_list = 9, 31, 6, [500, 300]
+    dg = DeviceGraph(g)
+    ch = Chains(dg, n_chains, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                base=case.base, seed=seed, chain_id0=id0)
+    ch.enable_sampled_waits()
+    ch.run(steps_list[0])
+    path_ck = str(tmp_path / "ck.npz")
+    ch.save_checkpoint(path_ck)
+    ch.run(steps_list[1])
+    got, st = ch.waits(), ch.stats()
+    ch2 = Chains.from_checkpoint(dg, path_ck, case.k, pop_bounds=case.bounds)
+    ch2.run(steps_list[1])
+    assert got.tobytes() == ch2.waits().tobytes()
+    pt = wait_prob_table(g.n, case.k)
+    lo, hi = case.bounds
+    for i in range(n_chains):
+        lab, ost, w = case.init.copy(), O.new_stats(1), O.Waits(pt)
+        for s in steps_list:
+            lab, ost, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, case.thr, seed, id0 + i,
+                                         s, stats=ost, waits=w)
+        assert np.array([w.sum, w.cur]).tobytes() == got[i].tobytes(), (name, i, w.sum, got[i])
+        assert_stats_equal(st[i:i + 1], ost)
+    assert (got[:, 0] > 0).all()
+
+
+def test_sampled_waits_big_grids(gpu_lib, monkeypatch):
+    """Sampled waits on the large-grid plans: the grid kernel's (200x200, k=4) and the
+    one-chain-per-wave kernel's (200x200, k=8, C5's), where p = |B|/(N^8 - 1) ~ 1e-33 (the
+    reference's int64 draw overflows there; the fp64 inversion does not)."""
+    from flipcomplexityempirical_amd.chain import (metropolis_table, population_bounds,
+                                                   wait_prob_table)
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    g = grid_graph(200, 200)
+    for k, bw in ((4, 2), (8, 4)):
+        init = block_seed(200, 200, 2, bw)
+        bounds = population_bounds(g.total_pop, k, 0.05)
+        dg = DeviceGraph(g)
+        ch = Chains(dg, 5, k, init, proposal="pairs", pop_bounds=bounds, base=0.5, seed=4)
+        ch.enable_sampled_waits()
+        ch.run(400)
+        got = ch.waits()
+        pt = wait_prob_table(g.n, k)
+        for i in range(5):
+            w = O.Waits(pt)
+            O.run_chain(g, init, k, 1, *bounds, metropolis_table(0.5, 4), 4, i, 400, waits=w)
+            assert np.array([w.sum, w.cur]).tobytes() == got[i].tobytes(), (k, i)
+        assert np.isfinite(got).all() and (got[:, 0] > 0).all()

@@ -142,3 +142,40 @@ def test_kansas_mean_wait_matches_reference(key, T):
         zs.append(z)
         assert abs(z) < 3.5, (key, u, bl, o.mean(), r.mean(), se)
     assert float(np.mean(np.square(zs))) < 2.5, (key, zs)
+
+
+@pytest.mark.parametrize("base,label", [(1.0, 100), (0.1, 10)])
+def test_sec11_sampled_wait_spread_matches_reference(base, label):
+    """The sampled form of geom_wait (one geometric inversion draw per state object,
+    re-used on re-yield: grid_chain_sec11.py:147-148,368,410-411; oracle wait_draw) on the
+    reference's own 15 sec11 runs (3 seed alignments x 5 tolerances, 100,000 yields): the
+    mean wait per yield within 3 combined standard errors of New_plots/sec11/*wait.txt, and
+    the run-to-run spread by a two-sided F test (alpha 0.002, 14 / 14 df).  At these bases
+    most of the reference's spread (CV 0.5-1.4%) is the geometric draws' own noise, which the
+    Rao-Blackwellised sum removes; the sampled sums must carry it."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from scipy import stats as S
+
+    from flipcomplexityempirical_amd.chain import wait_prob_table
+    ref = json.load(open(os.path.join(GOLDEN, "wait_sec11.json")))
+    refv = np.array([r["wait_sum"] / 1e5 for r in ref if r["base_label"] == label])
+    assert len(refv) == 15
+    g = sec11_graph()
+    pt = wait_prob_table(g.n, 2)
+
+    def one(run):
+        a, pop = run
+        lo, hi = population_bounds(g.n, 2, pop)
+        w = O.Waits(pt)
+        _, st, _, _ = O.run_chain(g, sec11_seed(g, a), 2, 0, lo, hi,
+                                  metropolis_table(base, g.maxdeg), 7, a * 10 + int(pop * 100),
+                                  99999, waits=w)
+        return w.sum / st["yields"][0]
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        ours = np.array(list(ex.map(one, [(a, p) for a in (0, 1, 2) for p in POPS])))
+    se = np.sqrt(refv.var(ddof=1) / 15 + ours.var(ddof=1) / 15)
+    assert abs(ours.mean() - refv.mean()) < 3 * se, (ours.mean(), refv.mean(), se)
+    F = ours.var(ddof=1) / refv.var(ddof=1)
+    assert S.f.ppf(0.001, 14, 14) < F < S.f.ppf(0.999, 14, 14), (F, ours.std(), refv.std())
