@@ -461,9 +461,11 @@ void fw_chains_destroy(fw_chains* c) {
   delete c;
 }
 
-// work units per slice: the grid kernel's quads (four chains per wave), else chains
+// work units per slice: the grid kernel's chains per wave (4 / rows per chain), else chains
 static long long slice_units(const fw_chains* c) {
-  return c->p.use16 ? (c->n_chains + 3) / 4 : c->n_chains;
+  if (!c->p.use16) return c->n_chains;
+  const int cpw = 4 / fw_grid16_launch_rows(c->p);
+  return (c->n_chains + cpw - 1) / cpw;
 }
 
 int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* init_labels,
@@ -599,6 +601,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.thr_stride = thr_per_chain ? 2 * D + 1 : 0;
   p.lb = lb;
   p.use16 = use16 ? 1 : 0;
+  p.spec = 1;
   if ((use16 ? fw_grid16_plan(p, g->device, &c->grid)
              : fw_run_grid_size(p, lb, g->device, &c->grid)) != 0) {
     delete c;
@@ -654,7 +657,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.spill = c->d_spill;
   p.next_chain = c->d_next;
   p.slices = 1;
-  if (hipMalloc(&c->d_segdone, sizeof(int32_t) * (size_t)slice_units(c)) != hipSuccess) {
+  // one per chain: enough for every kernel's work units (quads, pairs or chains)
+  if (hipMalloc(&c->d_segdone, sizeof(int32_t) * (size_t)n_chains) != hipSuccess) {
     fw_chains_destroy(c);
     return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
   }
@@ -681,7 +685,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
 static int launch_slices(const fw_chains* c, int64_t steps) {
   const char* e = getenv("FLIPWALK_SLICES");
   const int force = e && e[0] ? atoi(e) : 0;
-  const long long nq = slice_units(c), W = (long long)c->grid * (c->p.use16 ? c->p.nw : 1);
+  const long long nq = slice_units(c), W = (long long)c->grid * (c->p.use16 ? fw_grid16_launch_nw(c->p) : 1);
   // the kernels number units in int32: nq * S stays below 2^31
   const long long s_max = std::max<long long>(1, std::min<long long>(8, 0x7FFFFFFFll / std::max(nq, 1ll)));
   if (force >= 1) return (int)std::min<long long>({(long long)force, std::max<int64_t>(steps, 1), s_max});

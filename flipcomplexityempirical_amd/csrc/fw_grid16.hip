@@ -24,6 +24,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "fw_device.h"
 
 #ifdef FW_STAMPS
@@ -440,6 +442,29 @@ __device__ int grid_race_bb_row(const LDS uint8_t* lab, int n, int W, int H, int
   return verdict;
 }
 
+// value of lane L (any lane of the wave; every lane must execute it)
+__device__ __forceinline__ uint32_t lane_read(uint32_t x, int L) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(L << 2, (int)x);
+}
+// speculative attempts (R rows per chain): the sum of x over the R rows of this lane's group
+// (row-lane q of each), every lane of the group getting it
+template <int R>
+__device__ __forceinline__ uint32_t grp_sum(uint32_t x, int gb, int q) {
+  uint32_t t = 0;
+#pragma unroll
+  for (int s = 0; s < R; ++s) t += lane_read(x, gb + s * ROW + q);
+  return t;
+}
+template <int R>
+__device__ __forceinline__ uint64_t grp_sum64(uint64_t x, int gb, int q) {
+  uint64_t t = 0;
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    t += (uint64_t)lane_read((uint32_t)x, gb + s * ROW + q) |
+         ((uint64_t)lane_read((uint32_t)(x >> 32), gb + s * ROW + q) << 32);
+  return t;
+}
+
 // 4-bit scratch field x := 0 (atomic on the shared word)
 __device__ __forceinline__ void scr_clear(LDS uint8_t* scr, int x) {
   __atomic_fetch_and(PK<4>::word(scr, x), ~(15u << PK<4>::shift(x)), __ATOMIC_RELAXED);
@@ -565,13 +590,30 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
 // nodes) are scanned first (PER per lane), then the 16 group sums of the chosen supergroup
 // (one per lane), then the 64 nodes of the group — and labels take 3 bits when k <= 8,
 // so that two waves (eight 40,000-node chains) fit one CU's LDS.
-template <int LB, int MODE, int PER, bool FULL, bool BIG>
-__global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
+//
+// R (speculative attempts, lean small-grid instantiations only): R rows of a wavefront
+// work on ONE chain, 4/R chains per wave.  Row s of a chain's group evaluates proposal
+// attempt t + s on the same state; the group then consumes attempts in order up to and
+// including the first one that changes the state (valid and accepted), so attempts after
+// it are discarded and drawn again from the new state.  The state changes only on an
+// accepted flip, so every consumed evaluation is the one the sequential chain makes and
+// trajectories, counters and sums stay bit-identical.  It raises the attempts per chain
+// per wave iteration (C3: 1.56 at R = 2, 2.05 at R = 4) where too few chains are left to
+// fill the GPU: an 8,192-chain shard leaves a third of the wave slots empty at R = 1.
+template <int LB, int MODE, int PER, bool FULL, bool BIG, int R>
+__device__ __forceinline__ void grid16_body(const FwRunParams& p) {
   static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
+  static_assert(R == 1 || R == 2 || R == 4, "rows per chain");
+  static_assert(R == 1 || (!FULL && !BIG), "speculation: lean small-grid kernels only");
+  constexpr int CPW = 4 / R;  // chains per wavefront
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ int32_t s_lock;
   using P = PK<LB>;
   const int lane = __lane_id(), row = lane >> 4, q = lane & 15;
+  const int sx = row & (R - 1);     // speculation index of this row within its chain's group
+  const int grp = row / R;          // the chain of this row within the wave
+  const int gb = grp * R * ROW;     // first lane of the group
+  const bool owner = sx == 0;       // the row that keeps the chain's observations
   const int wv = (int)(threadIdx.x >> 6);
   // grid shape and bounds live in VGPRs: the hot loop uses them only in vector ops, and
   // the scalar file is the scarce one (SGPR spills cost v_readlane round trips)
@@ -581,7 +623,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   const int k = (int)in_vgpr((uint32_t)p.k);
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
   // this row's chain slot (after a 16-B guard: lab_window may read the word before a slot)
-  LDS uint8_t* const lab = sm + LDS_GUARD + (wv * 4 + row) * p.slot_stride;
+  LDS uint8_t* const lab = sm + LDS_GUARD + (wv * CPW + grp) * p.slot_stride;
   LDS uint32_t* const gsum = reinterpret_cast<LDS uint32_t*>(lab + p.off_gsum);  // u16 pairs
   // BIG: supergroup sums (u16 pairs, the level-1 array); otherwise level 1 reads gsum
   LDS uint32_t* const ssum = reinterpret_cast<LDS uint32_t*>(lab + p.off_ssum);
@@ -645,7 +687,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   // quad's previous slice is written back (seg_done, agent-scope release / acquire: the
   // previous slice ran a round or more earlier, so the wait is normally already over); the
   // trajectory equals separate launches of the slices' step counts.
-  const int nq = (p.n_chains + 3) >> 2;
+  const int nq = (p.n_chains + CPW - 1) / CPW;
   for (;;) {
     int cb = 0;
     if (lane == 0) cb = atomicAdd(p.next_chain, 1);
@@ -667,8 +709,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     UNIT_TIME(u, 0);
-    const int cbase = quad * 4;
-    const int c = cbase + row;
+    const int cbase = quad * CPW;
+    const int c = cbase + grp;
     const bool has = c < p.n_chains;
     const int cc = has ? c : cbase;  // a valid index for loads of absent rows
     const uint64_t gid = (uint64_t)(p.chain_id0 + c);
@@ -680,7 +722,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(lab);
       // with a valid derived-state cache the slot's group sums come along (see lab_copy16)
       const int nv = cached ? p.lab_copy16 : p.lab_bytes / 16;
-      for (int i = q; i < nv; i += ROW) dst[i] = src[i];
+      for (int i = sx * ROW + q; i < nv; i += R * ROW) dst[i] = src[i];
     }
     int32_t pops = q < k ? (int32_t)p.pops[(size_t)cc * k + q] : 0;  // total pop < 2^31
     double thr_l = FULL && q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
@@ -717,6 +759,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     uint32_t n_steps = 0, n_acc = 0, n_popf = 0, n_conf = 0, n_sdeg = 0, n_adeg = 0, n_bchg = 0;
     uint32_t retries = 0;
     uint64_t n_bfs = 0, n_bfsn = 0, n_bfsd = 0;
+    uint32_t bpos_w = ROW * R;  // R > 1: next unconsumed attempt of the group's Philox batch
     Pend pend = maps_on ? pend_load(p, cc) : Pend{-1, 0, 0u};
     // boundary_node-flagged nodes of district q (FW_ACCEPT_BOUNDARY), lane q
     int32_t bcnt = rule == FW_ACCEPT_BOUNDARY && q < k ? p.bcnt[(size_t)cc * k + q] : 0;
@@ -833,7 +876,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       hb1 += ib == q + ROW;
     };
     if (waits_on && first) wcur = wait_draw(p.seed, FW_WAIT_T0, gid, p.wlp[bnodes]);
-    observe(first);
+    observe(first && owner);
 
     // Philox batches: lane q of a row holds the draw of its chain's attempt (base + q).
     // Active rows consume one attempt per loop iteration in lockstep: each iteration
@@ -868,26 +911,53 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         else __builtin_amdgcn_s_setprio(0);
       }
 
-      if (bpos == ROW) {
-        if (n_sdeg >= p.fold_at) {  // rare: fold (see att0); one row at a time
-          if (q == 0 && has) {
-            stp->pop_fail += n_popf;
-            stp->contig_fail += n_conf;
-            stp->sum_deg += n_sdeg;
+      U4 x;
+      if constexpr (R == 1) {
+        if (bpos == ROW) {
+          if (n_sdeg >= p.fold_at) {  // rare: fold (see att0); one row at a time
+            if (q == 0 && has) {
+              stp->pop_fail += n_popf;
+              stp->contig_fail += n_conf;
+              stp->sum_deg += n_sdeg;
+            }
+            att0 += n_att;
+            n_att = n_popf = n_conf = n_sdeg = 0;
           }
-          att0 += n_att;
-          n_att = n_popf = n_conf = n_sdeg = 0;
+          const uint64_t t = att0 + (uint64_t)(n_att + (uint32_t)q);
+          pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
+                      in_vgpr(key0), in_vgpr(key1));
+          bpos = 0;
         }
-        const uint64_t t = att0 + (uint64_t)(n_att + (uint32_t)q);
-        pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
-                    in_vgpr(key0), in_vgpr(key1));
-        bpos = 0;
+        // lane 0 of the row holds this attempt's draw; shift the batch for the next one
+        x = U4{row_first(pb.x0), row_first(pb.x1), row_first(pb.x2), row_first(pb.x3)};
+        pb = U4{row_shl1(pb.x0), row_shl1(pb.x1), row_shl1(pb.x2), row_shl1(pb.x3)};
+        ++bpos;
+        n_att += act ? 1u : 0u;
+      } else {
+        // the group's R rows hold 16 R consecutive attempts (row s: base + 16 s + q); row s
+        // takes attempt bpos_w + s; refilled from the next unconsumed attempt when fewer
+        // than R are left
+        if (bpos_w > (uint32_t)(ROW * R - R)) {
+          if (4u * n_att >= p.fold_at) {  // rare (grids: degree <= 4): fold, group-uniform
+            const uint32_t f0 = grp_sum<R>(n_popf, gb, q), f1 = grp_sum<R>(n_conf, gb, q);
+            const uint32_t f2 = grp_sum<R>(n_sdeg, gb, q);
+            if (q == 0 && owner && has) {
+              stp->pop_fail += f0;
+              stp->contig_fail += f1;
+              stp->sum_deg += f2;
+            }
+            att0 += n_att;
+            n_att = n_popf = n_conf = n_sdeg = 0;
+          }
+          const uint64_t t = att0 + (uint64_t)(n_att + (uint32_t)(sx * ROW + q));
+          pb = philox((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid, (uint32_t)(gid >> 32),
+                      in_vgpr(key0), in_vgpr(key1));
+          bpos_w = 0;
+        }
+        const int srcl = gb + (int)bpos_w + sx;
+        x = U4{lane_read(pb.x0, srcl), lane_read(pb.x1, srcl), lane_read(pb.x2, srcl),
+               lane_read(pb.x3, srcl)};
       }
-      // lane 0 of the row holds this attempt's draw; shift the batch for the next one
-      const U4 x = {row_first(pb.x0), row_first(pb.x1), row_first(pb.x2), row_first(pb.x3)};
-      pb = U4{row_shl1(pb.x0), row_shl1(pb.x1), row_shl1(pb.x2), row_shl1(pb.x3)};
-      ++bpos;
-      n_att += act ? 1u : 0u;
       const uint32_t r = scale64(x.x0, x.x1, (uint32_t)(npairs > 0 ? npairs : 1));
 
       STAMP(0);  // draw
@@ -964,7 +1034,8 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const uint32_t pk2 = row_pick(((uint32_t)(q * 4 + t2) << 16) | ((r2 - bef2) & 0xFFFFu), L2, q);
       const int v = min(gi * 64 + (int)(pk2 >> 16), n - 1);
       const uint32_t j = pk2 & 0xFFFFu;
-      if (act && (rb1 == 0 || rb2 == 0 || rbg == 0)) stuck = 2;  // inconsistent: flag, stop
+      // inconsistent sums: flag, stop (R > 1: if the attempt is consumed, in the merge)
+      if (R == 1 && act && (rb1 == 0 || rb2 == 0 || rbg == 0)) stuck = 2;
       const bool go = act && rb1 != 0 && rb2 != 0 && rbg != 0;
 
       STAMP(2);  // level 2
@@ -1100,6 +1171,28 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       const uint64_t b_minus = ballot(go && mine && wo > 0 && wn == 0);
       const int plus = __popc(rowbits(b_plus, row)), minus = __popc(rowbits(b_minus, row));
       const double invb_new = p.g.invb[bnodes + plus - minus];
+      // R > 1: the Metropolis verdict is known before contiguity; an exact search is skipped
+      // when an earlier attempt of the same chain is known to change the state
+      bool wacc = false;
+      if constexpr (R > 1) {
+        const bool acc_l = (((uint64_t)(x.x2 >> 5) << 26) | (uint64_t)(x.x3 >> 6)) < thr53_l;
+        wacc = ((rowbits(ballot(acc_l), row) >> (dcut + D)) & 1u) != 0u;
+      }
+      // this attempt's exact search: runs, dequeued cells, their degrees (R > 1: counted
+      // only if the attempt is consumed; R = 1: straight into the unit's counters)
+      uint32_t it_bfs = 0;
+      uint64_t it_bfsn = 0, it_bfsd = 0;
+      auto count_search = [&](uint64_t bn_, uint64_t bd_) {
+        if constexpr (R == 1) {
+          n_bfs += 1;
+          n_bfsn += bn_;
+          n_bfsd += bd_;
+        } else {
+          it_bfs = 1;
+          it_bfsn = bn_;
+          it_bfsd = bd_;
+        }
+      };
       // ---- contiguity: 8-cell ring test, 7x7 window, exact race search when undecided
       const uint32_t rbits8 = rowbits(ballot(q >= 1 && q <= 8 && h.lx == a), row) >> 1;
       const int pN = rbits8 & 1, pW = (rbits8 >> 1) & 1, pE = (rbits8 >> 2) & 1, pS = (rbits8 >> 3) & 1;
@@ -1144,9 +1237,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (need && vb >= 0) {
           contig = vb == 1;
           need = false;
-          n_bfs += 1;
-          n_bfsn += bn16;
-          n_bfsd += bd16;
+          count_search(bn16, bd16);
         }
       }
       uint64_t rows_need = ballot(q == 0 && need);
@@ -1155,6 +1246,16 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         const int L0 = __ffsll((unsigned long long)rows_need) - 1;
         rows_need &= rows_need - 1;
         const int rr = L0 >> 4;
+        if constexpr (R > 1) {
+          if (rr % R) {  // an earlier attempt of this chain changes the state: discarded
+            const uint64_t sure = ballot(q == 0 && go && pop_ok && contig && wacc);
+            const uint32_t before = (uint32_t)((1u << (rr % R)) - 1u) << (rr - rr % R);
+            uint32_t rows_sure = 0;
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) rows_sure |= ((sure >> (16 * r4)) & 1u) << r4;
+            if (rows_sure & before) continue;
+          }
+        }
         const uint32_t aa = rdl(a, L0);
         const uint32_t am4 = rdl(amb, L0);
         const uint32_t lk = rdl((uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)), L0);
@@ -1166,9 +1267,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
         if (verdict >= 0) {
           if (row == rr) {
             contig = verdict == 1;
-            n_bfs += 1;
-            n_bfsn += bn;
-            n_bfsd += bd;
+            count_search(bn, bd);
           }
           continue;
         }
@@ -1212,9 +1311,7 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
                                       bd);
         if (row == rr) {
           contig = ok;
-          n_bfs += 1;
-          n_bfsn += bn;
-          n_bfsd += bd;
+          count_search(bn, bd);
         }
       }
       if (locked && lane == 0)
@@ -1223,6 +1320,89 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
       STAMP(4);  // exact searches
       // ---- outcome
       const bool valid = go && pop_ok && contig;
+      if constexpr (R > 1) {
+        // the group consumes its attempts in order up to the first state change (valid and
+        // accepted), the step limit or the retry limit; group-uniform, from row ballots
+        const bool accepted = valid && wacc;
+        const uint64_t b_go = ballot(q == 0 && go), b_val = ballot(q == 0 && valid);
+        const uint64_t b_acc = ballot(q == 0 && accepted);
+        uint32_t cons = 0, kold = 0, ns = n_steps, rt = retries;
+        int fpos = -1;
+        bool stop = !act;
+#pragma unroll
+        for (int s2 = 0; s2 < R; ++s2) {
+          const int L = gb + s2 * ROW;
+          const bool g2 = (b_go >> L) & 1ull, v2 = (b_val >> L) & 1ull, a2 = (b_acc >> L) & 1ull;
+          if (!stop && !g2) {  // inconsistent sums: flag, stop
+            stuck = 2;
+            stop = true;
+          }
+          if (!stop) {
+            cons = (uint32_t)s2 + 1u;
+            if (v2) {
+              ns += 1u;
+              rt = 0u;
+              if (a2) {
+                fpos = s2;
+                stop = true;
+              } else {
+                kold += 1u;
+              }
+              if (ns >= ustep) stop = true;
+            } else {
+              rt += 1u;
+              if (rt >= (uint32_t)p.max_retries) stop = true;
+            }
+          }
+        }
+        if (sx < (int)cons) {  // this row's attempt was consumed: its counters
+          n_sdeg += (uint32_t)dv;
+          if (!pop_ok) n_popf += 1;
+          else if (!contig) n_conf += 1;
+          n_bfs += it_bfs;
+          n_bfsn += it_bfsn;
+          n_bfsd += it_bfsd;
+        }
+        n_steps = ns;
+        retries = rt;
+        n_att += cons;
+        bpos_w += cons;
+        const bool commit_me = sx == fpos;
+        if (commit_me) {
+          n_acc += 1;
+          n_adeg += (uint32_t)dv;
+          n_bchg += (uint32_t)(plus + minus);
+          if (q == 0) P::axor(lab, v, a ^ d);
+          if (mine && wn != wo) lds_add(gsum + (h.x >> 7), (wn - wo) << (16 * ((h.x >> 6) & 1)));
+        }
+        lds_order();
+        uint32_t dl = commit_me && mine ? wn - wo : 0u;
+        dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x111, 0xF, 0xF, true);
+        dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x112, 0xF, 0xF, true);
+        dl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x114, 0xF, 0xF, true);
+        const int dnp = (int)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)dl, 0x154, 0xF, 0xF, false);
+        // the committing row's deltas, read by every row of its group (all lanes execute)
+        const int fsrc = gb + (fpos < 0 ? 0 : fpos) * ROW + q;
+        const uint32_t pk = (uint32_t)(dcut + 8) | ((uint32_t)plus << 4) | ((uint32_t)minus << 8) |
+                            (a << 12) | (d << 16) | ((uint32_t)(dnp + 64) << 20);
+        const uint32_t pkf = lane_read(pk, fsrc);
+        const uint64_t ib = (uint64_t)__double_as_longlong(invb_new);
+        const uint32_t ibl = lane_read((uint32_t)ib, fsrc), ibh = lane_read((uint32_t)(ib >> 32), fsrc);
+        // yields: the old state once per consumed valid attempt before the change, then the
+        // new state (the owner row keeps the chain's sums and histogram windows)
+        for (uint32_t i = 0; i < kold; ++i) observe(owner);
+        if (fpos >= 0) {
+          npairs += (int)((pkf >> 20) & 127u) - 64;
+          cut += (int)(pkf & 15u) - 8;
+          bnodes += (int)((pkf >> 4) & 15u) - (int)((pkf >> 8) & 15u);
+          invb = __longlong_as_double((long long)(((uint64_t)ibh << 32) | ibl));
+          if ((uint32_t)q == ((pkf >> 12) & 15u)) pops -= 1;  // lean kernel: unit populations
+          if ((uint32_t)q == ((pkf >> 16) & 15u)) pops += 1;
+          observe(owner);
+        }
+        STAMP(5);
+        continue;
+      }
       if (go) {
         n_sdeg += (uint32_t)dv;
         if (!pop_ok) n_popf += 1;
@@ -1314,8 +1494,19 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
     }
 
     STAMP(6);  // loop exit
-    // ---- write back
-    if (has) {
+    if constexpr (R > 1) {  // the row-local counters of the group, summed into every row
+      n_popf = grp_sum<R>(n_popf, gb, q);
+      n_conf = grp_sum<R>(n_conf, gb, q);
+      n_sdeg = grp_sum<R>(n_sdeg, gb, q);
+      n_acc = grp_sum<R>(n_acc, gb, q);
+      n_adeg = grp_sum<R>(n_adeg, gb, q);
+      n_bchg = grp_sum<R>(n_bchg, gb, q);
+      n_bfs = grp_sum64<R>(n_bfs, gb, q);
+      n_bfsn = grp_sum64<R>(n_bfsn, gb, q);
+      n_bfsd = grp_sum64<R>(n_bfsd, gb, q);
+    }
+    // ---- write back (R > 1: the owner row)
+    if (has && owner) {
       if (hc0) HIST_ADD(p.hist_cut + base_c + q, (unsigned long long)hc0);
       if (hc1) HIST_ADD(p.hist_cut + base_c + ROW + q, (unsigned long long)hc1);
       if (hb0) HIST_ADD(p.hist_b + base_b + q, (unsigned long long)hb0);
@@ -1372,6 +1563,19 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   STAMP_FLUSH
 }
 
+template <int LB, int MODE, int PER, bool FULL, bool BIG>
+__global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
+  grid16_body<LB, MODE, PER, FULL, BIG, 1>(p);
+}
+
+// speculative attempts: R rows per chain, a 4-waves-per-SIMD register budget (128 VGPRs),
+// since it is used where chains are too few for the R = 1 kernel's 3 waves per SIMD
+template <int LB, int MODE, int PER, int R>
+__global__ __launch_bounds__(64 * MAX_NW) __attribute__((amdgpu_waves_per_eu(4))) void
+fw_grid16_spec_kernel(FwRunParams p) {
+  grid16_body<LB, MODE, PER, false, false, R>(p);
+}
+
 // group sums per lane (PER) for G groups; BIG: supergroup sums per lane for G groups
 int per16(int G) { return G <= 16 * 2 ? 2 : G <= 16 * 4 ? 4 : G <= 16 * 10 ? 10 : 16; }
 int per16_big(int G) { return (G + 15) / 16 <= 32 ? 2 : 4; }
@@ -1398,6 +1602,27 @@ void* pick16(int G) {
       default: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL, false>);
     }
   }
+}
+
+template <int LB, int MODE, int R>
+void* pick16_spec(int G) {
+  if (is_big(G) || LB == 3) return nullptr;
+  switch (per16(G)) {
+    case 2: return reinterpret_cast<void*>(&fw_grid16_spec_kernel<LB, MODE, 2, R>);
+    case 4: return reinterpret_cast<void*>(&fw_grid16_spec_kernel<LB, MODE, 4, R>);
+    case 10: return reinterpret_cast<void*>(&fw_grid16_spec_kernel<LB, MODE, 10, R>);
+    default: return reinterpret_cast<void*>(&fw_grid16_spec_kernel<LB, MODE, 16, R>);
+  }
+}
+
+template <int R>
+void* pick16_spec_mode(const FwRunParams& p) {
+  const bool cut = p.mode == FW_PROPOSE_CUTEDGE;
+  if (p.lb == 2)
+    return cut ? pick16_spec<2, FW_PROPOSE_CUTEDGE, R>(p.G) : pick16_spec<2, FW_PROPOSE_PAIRS, R>(p.G);
+  if (p.lb == 4)
+    return cut ? pick16_spec<4, FW_PROPOSE_CUTEDGE, R>(p.G) : pick16_spec<4, FW_PROPOSE_PAIRS, R>(p.G);
+  return nullptr;
 }
 
 template <bool FULL>
@@ -1453,17 +1678,36 @@ bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop) {
 
 int fw_grid16_lb(int G, int k) { return k <= 4 ? 2 : (is_big(G) ? 3 : 4); }
 
+static bool grid16_full(const FwRunParams& p) {
+  return p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr || p.ring_n > 0 ||
+         p.trace != nullptr || p.g.pop != nullptr || p.wsamp != nullptr;
+}
+
+int fw_grid16_launch_rows(const FwRunParams& p) { return grid16_full(p) ? 1 : p.spec; }
+
+// waves per workgroup of a launch: the plan holds nw * 4 / spec chain slots per workgroup,
+// which the R = 1 kernels (FULL features on) fill with nw / spec waves of four chains
+int fw_grid16_launch_nw(const FwRunParams& p) { return p.nw * fw_grid16_launch_rows(p) / p.spec; }
+
+static void* grid16_fn_r(const FwRunParams& p, bool full, int R) {
+  if (full) return pick16_mode<true>(p);
+  if (R == 2) return pick16_spec_mode<2>(p);
+  if (R == 4) return pick16_spec_mode<4>(p);
+  return pick16_mode<false>(p);
+}
+
 void* fw_grid16_fn(const FwRunParams& p) {
-  const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
-                    p.ring_n > 0 || p.trace != nullptr || p.g.pop != nullptr ||
-                    p.wsamp != nullptr;
-  return full ? pick16_mode<true>(p) : pick16_mode<false>(p);
+  return grid16_fn_r(p, grid16_full(p), fw_grid16_launch_rows(p));
 }
 
 // LDS plan of the grid kernel: per chain slot [labels | u16 group sums], slot stride
 // 16 B mod 128 B so the four rows of a wave start on different banks; then the shared
-// 4-bit search scratch and visit list.  Picks the waves per workgroup (1..4) that keep
-// the most chains resident per CU (ties: fewer waves).
+// 4-bit search scratch and visit list.  Picks the rows per chain R (speculative attempts,
+// grid16_body) and the waves per workgroup (1..4) that maximise a throughput model: chains
+// in flight (resident waves x 4/R, at most the chains there are) x the attempts a chain
+// consumes per wave iteration, E(R) = 1 + q + ... + q^(R-1) with q = 0.56 the probability
+// that an attempt leaves the state unchanged (C3), x 0.9 for R > 1 (its 128-VGPR budget and
+// the merge).  Ties: R = 1, then fewer waves.  FLIPWALK_SPEC=1/2/4 forces R.
 int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   // slot: labels | u16 group sums (16 x PER per row; BIG: padded to whole supergroups) |
   // BIG: u16 supergroup sums (16 x PER)
@@ -1478,40 +1722,73 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   p.off_ssum = p.off_gsum + gbytes;
   p.scr_bytes = round16i((p.g.n + 1) / 2 + 8);
   if (p.qcap16 <= 0) p.qcap16 = 384;
-  void* fn = fw_grid16_fn(p);
-  if (!fn) return -1;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
-  int best_nw = 0, best_chains = 0, best_lds = 0;
-  for (int nw = 1; nw <= MAX_NW; ++nw) {
-    const int lds = LDS_GUARD + 4 * nw * stride + p.scr_bytes + 4 * p.qcap16;
-    if (lds > 160 * 1024 - 256) break;
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-      return -1;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nw, (size_t)lds) !=
-        hipSuccess)
-      return -1;
-    if (per_cu * 4 * nw > best_chains) {
-      best_chains = per_cu * 4 * nw;
-      best_nw = nw;
-      best_lds = lds;
+  const char* es = getenv("FLIPWALK_SPEC");
+  const int force = es && es[0] ? atoi(es) : 0;
+  const bool full = grid16_full(p);
+  const bool spec_ok = !big && (p.lb == 2 || p.lb == 4) && !full;
+  double best_score = -1.0;
+  int best_nw = 0, best_r = 1, best_blocks = 0, best_lds = 0;
+  for (int R = 1; R <= 4; R *= 2) {
+    if (R > 1 && !spec_ok) break;
+    if (force && force != R) continue;
+    void* fn = grid16_fn_r(p, full, R);
+    if (!fn) return -1;
+    const int cpw = 4 / R;
+    // waves per workgroup for this R: the most resident waves per CU (ties: fewer)
+    int r_nw = 0, r_blocks = 0, r_lds = 0;
+    for (int nw = R; nw <= MAX_NW; ++nw) {
+      if (nw % R) continue;  // the R = 1 kernels must fill the same slots (fw_grid16_launch_nw)
+      const int lds = LDS_GUARD + cpw * nw * stride + p.scr_bytes + 4 * p.qcap16;
+      if (lds > 160 * 1024 - 256) break;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+        return -1;
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nw, (size_t)lds) !=
+          hipSuccess)
+        return -1;
+      if (per_cu * nw > r_blocks * r_nw) {
+        r_nw = nw;
+        r_blocks = per_cu;
+        r_lds = lds;
+      }
+    }
+    if (r_nw == 0) continue;
+    const double e_r = R == 1 ? 1.0 : (R == 2 ? 1.56 : 1.0 + 0.56 + 0.56 * 0.56 + 0.56 * 0.56 * 0.56);
+    const double eff = R == 1 ? 1.0 : 0.9;
+    const double waves = (double)r_blocks * r_nw * prop.multiProcessorCount;
+    const double units = (double)((p.n_chains + cpw - 1) / cpw);
+    const double score = std::min(units, waves) * cpw * e_r * eff;
+    if (score > best_score * (1.0 + 1e-9)) {
+      best_score = score;
+      best_nw = r_nw;
+      best_r = R;
+      best_blocks = r_blocks;
+      best_lds = r_lds;
     }
   }
   if (best_nw == 0) return -1;
+  p.spec = best_r;
   p.nw = best_nw;
-  p.off_scr = LDS_GUARD + 4 * best_nw * stride;
+  const int cpw = 4 / best_r;
+  p.off_scr = LDS_GUARD + cpw * best_nw * stride;
   p.off_list16 = p.off_scr + p.scr_bytes;
   p.lds16 = best_lds;
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, best_lds) != hipSuccess)
-    return -1;
+  // both the lean kernel of the plan and the FULL one (features switched on later)
+  for (int f = 0; f < 2; ++f) {
+    void* fn = grid16_fn_r(p, f == 1, f == 1 ? 1 : best_r);
+    if (fn && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, best_lds) != hipSuccess)
+      return -1;
+  }
   const char* verbose = getenv("FLIPWALK_VERBOSE");
   if (verbose && verbose[0] == '1')
-    fprintf(stderr, "flipwalk: grid kernel %s, %d-bit labels, LDS %d B per workgroup of %d waves, "
-            "%d chains per CU\n", is_big(p.G) ? "large-grid plan" : "small-grid plan", p.lb,
-            best_lds, best_nw, best_chains);
-  const long long per_wg = 4LL * best_nw;
-  long long gsz = (long long)(best_chains / per_wg) * prop.multiProcessorCount;
+    fprintf(stderr, "flipwalk: grid kernel %s, %d-bit labels, %d row(s) per chain, LDS %d B per "
+            "workgroup of %d waves, %d workgroups (%d chains) per CU\n",
+            is_big(p.G) ? "large-grid plan" : "small-grid plan", p.lb, best_r, best_lds, best_nw,
+            best_blocks, best_blocks * best_nw * cpw);
+  const long long per_wg = (long long)cpw * best_nw;
+  long long gsz = (long long)best_blocks * prop.multiProcessorCount;
   const long long need = (p.n_chains + per_wg - 1) / per_wg;
   if (gsz > need) gsz = need;
   *grid = (int)(gsz < 1 ? 1 : gsz);
@@ -1524,6 +1801,6 @@ int fw_grid16_launch(const FwRunParams& p, int grid, void* stream) {
   if (!fn) return (int)hipErrorInvalidDeviceFunction;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds16);
   if (e != hipSuccess) return (int)e;
-  return (int)hipLaunchKernel(fn, dim3(grid), dim3(64 * p.nw), args, (size_t)p.lds16,
-                              (hipStream_t)stream);
+  return (int)hipLaunchKernel(fn, dim3(grid), dim3(64 * fw_grid16_launch_nw(p)), args,
+                              (size_t)p.lds16, (hipStream_t)stream);
 }

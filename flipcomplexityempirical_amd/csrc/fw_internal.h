@@ -69,7 +69,8 @@ struct FwRunParams {
   int32_t use16;               // 1: launch the four-chains-per-wave grid kernel
   // grid kernel LDS plan (fw_grid16_plan): 4*nw chain slots, shared scratch and list
   int32_t slot_stride;         // bytes between chain slots
-  int32_t nw;                  // waves per workgroup
+  int32_t nw;                  // waves per workgroup (of the plan's lean kernel)
+  int32_t spec;                // rows per chain of the lean kernel (speculative attempts: 1, 2, 4)
   int32_t off_scr, scr_bytes;  // 4-bit search scratch
   int32_t off_list16, qcap16;  // shared visit list
   int32_t no_bb;               // 1: exact searches skip the bitboard form (tests)
@@ -167,3 +168,5 @@ int fw_grid16_lb(int G, int k);
 void* fw_grid16_fn(const FwRunParams& p);
 int fw_grid16_plan(FwRunParams& p, int device, int* grid);
 int fw_grid16_launch(const FwRunParams& p, int grid, void* stream);
+int fw_grid16_launch_rows(const FwRunParams& p);  // rows per chain of the kernel launched
+int fw_grid16_launch_nw(const FwRunParams& p);    // waves per workgroup of that kernel

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Speculative attempts: parity tests, then A/B lines (FLIPWALK_SPEC=1 vs the host's pick) on
+# the 8-GPU C3 shard and C2; then the C5 steady-state stamps.  Output under gpurun_out/r03c/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r03c
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "speculative or stuck or chain_bit_exact" > $O/pytest_spec.log 2>&1
+rc=$?
+grep -E "passed|failed" $O/pytest_spec.log | tail -2
+grep -E "FAILED|^E " $O/pytest_spec.log | head -20
+if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
+: > $O/ab_spec.jsonl
+for rep in 1 2; do
+for cfg in "--shard 0/8" "--config c2" "--shard 0/4"; do
+  for sp in 1 auto; do
+    if [ $sp = auto ]; then unset FLIPWALK_SPEC; else export FLIPWALK_SPEC=$sp; fi
+    FLIPWALK_VERBOSE=1 timeout -k 10 200 python -u bench.py $cfg --steps 20 --warmup 5 --no-cpu-baseline --check-chains 4 >> $O/ab_spec.jsonl 2> $O/ab_spec.err || { echo "bench $cfg $sp failed"; tail -5 $O/ab_spec.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/ab_spec.jsonl').read().splitlines()[-1]); print('$cfg spec=$sp', '%.4g' % d['value'], 'kernel_ms=%.3f' % d['kernel_ms'], d['parity_check']['equal'], '/', d['parity_check']['chains'])"
+    grep "grid kernel" $O/ab_spec.err | tail -1
+  done
+done
+done
+unset FLIPWALK_SPEC
+timeout -k 10 200 python -u scripts/stamps.py c5 8192 10 > $O/stamps_c5_warm10.txt 2>&1 || { echo "stamps warm10 failed"; tail -5 $O/stamps_c5_warm10.txt; exit 1; }
+cat $O/stamps_c5_warm10.txt
+timeout -k 10 300 python -u scripts/stamps.py c5 8192 60 > $O/stamps_c5_warm60.txt 2>&1 || { echo "stamps warm60 failed"; tail -5 $O/stamps_c5_warm60.txt; exit 1; }
+cat $O/stamps_c5_warm60.txt

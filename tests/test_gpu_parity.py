@@ -708,3 +708,68 @@ def test_sampled_waits_big_grids(gpu_lib, monkeypatch):
             O.run_chain(g, init, k, 1, *bounds, metropolis_table(0.5, 4), 4, i, 400, waits=w)
             assert np.array([w.sum, w.cur]).tobytes() == got[i].tobytes(), (k, i)
         assert np.isfinite(got).all() and (got[:, 0] > 0).all()
+
+
+SPEC_GRIDS = ["grid10_k2_bi", "grid12_k4_pairs", "grid12_k4_cut", "grid20_k4_mu", "grid16x24_k8",
+              "grid7x9_k3_cut", "grid11x13_k4", "grid30x18_k2_bi"]
+SPEC_ENVS = {"plain": {}, "units": {"FLIPWALK_GRID_CAP": "1", "FLIPWALK_SLICES": "3"},
+             "fold": {"FLIPWALK_FOLD_AT": "64"}, "list": {"FLIPWALK_NO_BITBOARD": "1"},
+             "split": {"FLIPWALK_LAUNCH_STEPS": "97"}}
+SPEC_CASES = ([(n, r, "plain") for n in SPEC_GRIDS for r in ("2", "4")] +
+              [(n, r, e) for n in ("grid20_k4_mu", "grid16x24_k8") for r in ("2", "4")
+               for e in ("units", "fold", "list", "split")])
+
+
+@pytest.mark.parametrize("name,rows,env", SPEC_CASES, ids=[f"R{r}-{e}-{n}" for n, r, e in SPEC_CASES])
+def test_speculative_attempts_bit_exact(gpu_lib, name, rows, env, monkeypatch):
+    """The grid kernel with R rows per chain (FLIPWALK_SPEC=R: speculative attempts t .. t+R-1
+    on one state, consumed up to the first state change): plans, every counter, the fp64 sum
+    and the histograms equal the oracle's sequential chain, also with many work units per
+    wave and slices, early counter folds, list searches under the lock and split launches."""
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    monkeypatch.setenv("FLIPWALK_SPEC", rows)
+    for kk, vv in SPEC_ENVS[env].items():
+        monkeypatch.setenv(kk, vv)
+    case = {c.name: c for c in CASES}[name]
+    st = _run_vs_oracle(case, 37, [600, 250, 150])
+    assert (st["accepts"] > 0).all()
+
+
+@pytest.mark.parametrize("rows", ["2", "4"])
+def test_speculative_plan_runs_full_features(gpu_lib, rows, monkeypatch, tmp_path):
+    """A handle planned with R rows per chain that later switches on FULL features (the
+    |B'|/|B| rule, the ring observable, sampled waits) runs the R = 1 FULL kernel in the same
+    LDS slots; a stuck chain stops at exactly max_retries attempts under speculation."""
+    from flipcomplexityempirical_amd import shape
+    from flipcomplexityempirical_amd.chain import annealing_table, wait_prob_table
+    from flipcomplexityempirical_amd.graph import grid_graph, stripe_seed
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    monkeypatch.setenv("FLIPWALK_SPEC", rows)
+    case = {c.name: c for c in CASES}["grid20_k4_mu"]
+    g = case.graph
+    thr = annealing_table(0.9, 1, g.maxdeg)
+    dg = DeviceGraph(g)
+    ch = Chains(dg, 21, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds, seed=3,
+                thr=thr)
+    ch.run(300)  # lean, R rows per chain
+    ru, rw = shape.ring_edges(g, shape.grid_on_ring(20, 20))
+    ch.set_accept("bratio")
+    ch.enable_ring(ru, rw)
+    ch.run(200)  # FULL, one row per chain
+    ring = O.Ring(ru, rw)
+    labs, st = ch.labels(), ch.stats()
+    lo, hi = case.bounds
+    for i in range(21):
+        lab, ost = case.init.copy(), O.new_stats(1)
+        lab, ost, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, thr, 3, i, 300, stats=ost)
+        lab, ost, _, _ = O.run_chain(g, lab, case.k, case.mode, lo, hi, thr, 3, i, 200, stats=ost,
+                                     accept_rule=1, ring=ring)
+        assert np.array_equal(labs[i], lab), i
+        assert_stats_equal(st[i:i + 1], ost)
+    assert np.array_equal(ch.hist_ring(), ring.hist)
+    g6 = grid_graph(6, 6)
+    lab6 = stripe_seed(6, 6)
+    ch6 = Chains(DeviceGraph(g6), 4, 2, lab6, proposal="bi", pop_bounds=(18, 18), base=1.0)
+    ch6.run(10, max_retries=50)
+    st6 = ch6.stats()
+    assert st6["stuck"].all() and (st6["steps"] == 0).all() and (st6["attempts"] == 50).all()
