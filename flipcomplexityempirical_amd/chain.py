@@ -440,6 +440,7 @@ class RunResult:
     pops: np.ndarray        # [n_chains, k]
     kernel_ms: float
     maps: Optional[dict] = None  # spatial observables (Chains.read_map), per chain
+    waits: Optional[np.ndarray] = None  # sampled geom_wait sums per chain (Chains.sampled_waits)
 
     def expected_wait_sums(self, n_nodes: int, k: int) -> np.ndarray:
         return expected_wait_sum(self.stats, n_nodes, k)
@@ -457,12 +458,13 @@ def run_chains(graph: Graph, init_labels, k: int, n_chains: int, steps: int,
                proposal: str | int = "pairs", percent: float = 0.05, base=1.0, seed: int = 0,
                chain_id0: int = 0, device: int = 0, pop_bounds=None,
                max_retries: int = DEFAULT_MAX_RETRIES, total_steps: Optional[int] = None,
-               maps: bool = False, label_values=None) -> RunResult:
+               maps: bool = False, label_values=None, waits: bool = False) -> RunResult:
     """Run ``n_chains`` chains for ``steps`` counted steps each and read everything back.
 
     ``total_steps`` (GerryChain's meaning: yields including the initial state) may be
     given instead of ``steps``; then steps = total_steps - 1.  ``maps`` also returns the
-    driver's spatial observables (``label_values``: GerryChain values of districts 0..k-1).
+    driver's spatial observables (``label_values``: GerryChain values of districts 0..k-1);
+    ``waits`` the sampled geom_wait sums (grid_chain_sec11.py:147-148,410-411).
     """
     if total_steps is not None:
         steps = int(total_steps) - 1
@@ -471,9 +473,12 @@ def run_chains(graph: Graph, init_labels, k: int, n_chains: int, steps: int,
                 percent=percent, base=base, seed=seed, chain_id0=chain_id0)
     if maps:
         ch.enable_maps(label_values)
+    if waits:
+        ch.enable_sampled_waits()
     ch.run(steps, max_retries)
     res = RunResult(ch.labels(), ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(),
-                    ch.last_kernel_ms(), read_maps(ch) if maps else None)
+                    ch.last_kernel_ms(), read_maps(ch) if maps else None,
+                    ch.sampled_waits() if waits else None)
     ch.close()
     dg.close()
     return res

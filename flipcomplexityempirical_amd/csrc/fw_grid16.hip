@@ -1262,7 +1262,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
         uint64_t bn = 0, bd = 0;
         int verdict = -1;
         if (!p.no_bb)  // bitboard form first; the list search past its window
-          verdict = grid_race_bb<LB>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, n, W, H,
+          verdict = grid_race_bb<LB>(sm + LDS_GUARD + (wv * CPW + rr / R) * p.slot_stride, n, W, H,
                                     lane, rdl(vr, L0), rdl(vc, L0), aa, am4, lk, bn, bd);
         if (verdict >= 0) {
           if (row == rr) {
@@ -1306,7 +1306,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
         if (lk & 2) merge(sx(2), sx(3));  // E-S
         if (lk & 4) merge(sx(3), sx(1));  // S-W
         if (lk & 8) merge(sx(1), sx(0));  // W-N
-        const bool ok = grid_race<LB>(sm + LDS_GUARD + (wv * 4 + rr) * p.slot_stride, scr, list, spill,
+        const bool ok = grid_race<LB>(sm + LDS_GUARD + (wv * CPW + rr / R) * p.slot_stride, scr, list, spill,
                                       p.qcap16, W, H, gd, lane, vv, aa, mr, srcn, cls, bn,
                                       bd);
         if (row == rr) {

@@ -435,18 +435,24 @@ class MarkovChain:
     def __len__(self):
         return self.total_steps
 
-    def run_batched(self, n_chains: int, chain_id0: int = 0, maps: bool = False) -> RunResult:
+    def run_batched(self, n_chains: int, chain_id0: int = 0, maps: bool = False,
+                    waits: bool = False) -> RunResult:
         """n_chains independent copies for total_steps yields each (no per-state objects).
 
         ``maps`` adds the driver's spatial observables per chain, keyed by node / edge
         index (grid_chain_sec11.py:383-400, finalised as :416-419), with the initial
-        partition's own label values (e.g. -1/+1) in part_sum.
+        partition's own label values (e.g. -1/+1) in part_sum.  ``waits`` adds the sampled
+        sum(waits) of each chain (geom_wait, :147-148, written at :410-411), the value the
+        reference's wait.txt holds.
         """
         ch = self._make(n_chains, chain_id0)
         if maps:
             ch.enable_maps(np.asarray(self.initial_state._label_values, np.int64))
+        if waits:
+            ch.enable_sampled_waits()
         ch.run(self.total_steps - 1, self.max_retries)
         res = RunResult(ch.labels(), ch.stats(), ch.hist_cut(), ch.hist_b(), ch.pops(),
-                        ch.last_kernel_ms(), read_maps(ch) if maps else None)
+                        ch.last_kernel_ms(), read_maps(ch) if maps else None,
+                        ch.sampled_waits() if waits else None)
         ch.close()
         return res

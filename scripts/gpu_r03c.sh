@@ -20,8 +20,3 @@ for cfg in "--shard 0/8" "--config c2" "--shard 0/4"; do
   done
 done
 done
-unset FLIPWALK_SPEC
-timeout -k 10 200 python -u scripts/stamps.py c5 8192 10 > $O/stamps_c5_warm10.txt 2>&1 || { echo "stamps warm10 failed"; tail -5 $O/stamps_c5_warm10.txt; exit 1; }
-cat $O/stamps_c5_warm10.txt
-timeout -k 10 300 python -u scripts/stamps.py c5 8192 60 > $O/stamps_c5_warm60.txt 2>&1 || { echo "stamps warm60 failed"; tail -5 $O/stamps_c5_warm60.txt; exit 1; }
-cat $O/stamps_c5_warm60.txt
