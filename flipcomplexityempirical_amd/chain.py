@@ -19,6 +19,7 @@ them in Python:
 from __future__ import annotations
 
 import math
+import warnings
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -280,7 +281,18 @@ class Chains:
     def enable_ring(self, ring_u, ring_w) -> None:
         """Count yields per pair of first two cut ring edges (boundary_slope and the
         driver's slope / angle, grid_chain_sec11.py:55-78,371-394); ``shape.ring_edges``
-        builds the ring of a graph from the reference's predicates.  Zeroes the histogram."""
+        builds the ring of a graph from the reference's predicates.  Zeroes the histogram.
+
+        Parity holds for plans whose cut crosses the ring at most twice (k = 2 with both
+        districts connected: the reference's sec11 and Frankenstein runs).  With more
+        crossings the reference picks temp[0], temp[1] of ``list(set(...))`` (hash order),
+        this handle the first two in ring order, so k > 2 shape histograms are not
+        comparable with the reference's; a RuntimeWarning says so."""
+        if self.k > 2:
+            warnings.warn(f"enable_ring with k = {self.k}: plans can cut the ring more than "
+                          "twice, where the pair kept (first two in ring order) differs from "
+                          "the reference's set-order pick; shape parity holds for k = 2 only",
+                          RuntimeWarning, stacklevel=2)
         u = np.ascontiguousarray(ring_u, np.int32)
         w = np.ascontiguousarray(ring_w, np.int32)
         if u.shape != w.shape or u.ndim != 1:
