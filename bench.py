@@ -257,6 +257,12 @@ def main():
                     help="put every rank on GPU 0 (multi-rank rehearsal on a one-GPU box)")
     ap.add_argument("--maps", action="store_true",
                     help="also keep the spatial observables (cut_times, part_sum, ...) per chain")
+    ap.add_argument("--resume", default=None, metavar="NPZ",
+                    help="continue the chains of a --save-checkpoint file (same workload, seed "
+                         "and shard) instead of starting from the seed plan: steady-state "
+                         "timing and profiling without the burn-in launches")
+    ap.add_argument("--save-checkpoint", default=None, metavar="NPZ",
+                    help="write the chains (Chains.save_checkpoint) after the timed launches")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
                     help="per-launch HBM bytes from a rocprofv3 PMC pass of the default C3 "
                          "command (scripts/profile.sh -> scripts/pmc_summary.py)")
@@ -304,6 +310,14 @@ def main():
                 seed=args.seed, chain_id0=lo)
     if args.maps:
         ch.enable_maps([-1, 1] if k == 2 else None)
+    resumed = 0  # counted steps per chain already in the checkpoint
+    if args.resume:
+        from flipcomplexityempirical_amd.chain import STATS_DTYPE
+        ckf = np.load(args.resume, allow_pickle=False)
+        ck = {key: ckf[key] for key in ckf.files}
+        ck["stats"] = ckf["stats"].view(STATS_DTYPE)
+        ch.restore(ck)
+        resumed = int(ck["stats"]["steps"].max())
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -342,7 +356,7 @@ def main():
     pc = None
     if args.check_chains > 0:
         pc = parity_check(w, ch, bounds, base, args.seed, lo,
-                          (args.warmup + args.steps) * args.inner, args.check_chains,
+                          resumed + (args.warmup + args.steps) * args.inner, args.check_chains,
                           host_cores()[0])
         yields_local = int(st1_arr["yields"].astype(np.uint64).sum())
         if dist is not None:
@@ -357,6 +371,8 @@ def main():
         pc["hist_yields_equal"] = bool(int(hist_cut.sum()) == yields_all ==
                                        int(hist_b.sum()))
 
+    if args.save_checkpoint:
+        ch.save_checkpoint(args.save_checkpoint)
     kernel_ms = float(np.mean(kms))
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
@@ -418,6 +434,7 @@ def main():
                 "ladder": args.ladder if w.base is None else None,
                 "spatial_maps": bool(args.maps),
                 "flip_steps_per_chain_per_step": args.inner,
+                "resumed_steps_per_chain": resumed,
                 "parallelism": par,
                 "flipwalk_env": flipwalk_env(),
             },

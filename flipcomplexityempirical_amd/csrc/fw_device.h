@@ -542,6 +542,134 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
   return verdict;
 }
 
+// grid_race_bb on a 64-row x 64-column window: lane i = grid row vr - 32 + i, bit b of
+// dword w = column vc - 32 + 32 w + b, two VGPRs per set.  The same sets, levels, merges,
+// stopping rules and counters; a window-edge frontier returns -1 as there.  Used by the
+// one-chain-per-wave kernel on large grids (C5), whose steady-state searches leave the
+// 32-column window in a quarter of the runs and the 64-column one in 5% (200x200, k=8,
+// base 0.1 after 30,000 steps: scripts/search_stats.c).
+template <int LB>
+__device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int lane, int vr,
+                             int vc, uint32_t a, uint32_t am4, uint32_t lk, uint64_t& bfs_nodes,
+                             uint64_t& bfs_deg) {
+  const int r = vr - 32 + lane, c0 = vc - 32;
+  const bool rin = (r >= 0) & (r < H);
+  const int rowb = (rin ? r : vr) * W + c0;
+  // bits of columns cb .. cb + 31 inside [0, W)
+  auto colmask = [W](int cb) -> uint32_t {
+    uint32_t mk = cb <= -32 ? 0u : (cb < 0 ? ~0u << (-cb) : ~0u);
+    const int hi = W - cb;
+    if (hi < 32) mk &= hi <= 0 ? 0u : (1u << hi) - 1u;
+    return mk;
+  };
+  uint32_t A0 = eq_bits32<LB>(lab, n, rowb, a), A1 = eq_bits32<LB>(lab, n, rowb + 32, a);
+  A0 &= rin ? colmask(c0) : 0u;
+  A1 &= rin ? colmask(c0 + 32) : 0u;
+  if (lane == 32) A1 &= ~1u;  // v
+  // window-edge cells with an on-grid neighbour outside the window
+  const uint32_t er = ((lane == 0) & (r > 0)) | ((lane == 63) & (r < H - 1)) ? ~0u : 0u;
+  uint32_t E0 = er, E1 = er;
+  if (c0 > 0) E0 |= 1u;
+  if (c0 + 63 < W - 1) E1 |= 1u << 31;
+  E0 &= A0;
+  E1 &= A1;
+  // frontier per direction; sources up (31, 32), left (32, 31), right (32, 33), down (33, 32)
+  uint32_t F0[4], F1[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int sl = d == 0 ? 31 : (d == 3 ? 33 : 32);
+    const bool on = lane == sl && ((am4 >> d) & 1u);
+    F0[d] = on && d == 1 ? 0x80000000u : 0u;
+    F1[d] = on && d != 1 ? (d == 2 ? 2u : 1u) : 0u;
+  }
+  uint32_t M = 0x8421u;  // class of direction d: 4-bit member mask at bits 4d (uniform)
+  auto unite = [&](int i, int j) {
+    const uint32_t m = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if ((m >> d) & 1u) M = (M & ~(15u << (4 * d))) | (m << (4 * d));
+  };
+  if (lk & 1u) unite(0, 2);  // N-E
+  if (lk & 2u) unite(2, 3);  // E-S
+  if (lk & 4u) unite(3, 1);  // S-W
+  if (lk & 8u) unite(1, 0);  // W-N
+  auto n_classes = [&]() {
+    int nc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      nc += (int)(((am4 >> d) & 1u) && (__ffs((M >> (4 * d)) & 15u) - 1) == d);
+    return nc;
+  };
+  uint32_t V0 = F0[0] | F0[1] | F0[2] | F0[3], V1 = F1[0] | F1[1] | F1[2] | F1[3];
+  int verdict = -1;
+  uint32_t P0, P1;  // processed cells
+  for (;;) {
+    const uint32_t l0 = F0[0] | F0[1] | F0[2] | F0[3], l1 = F1[0] | F1[1] | F1[2] | F1[3];
+    if (n_classes() == 1) {
+      verdict = 1;
+      P0 = V0 & ~l0;
+      P1 = V1 & ~l1;
+      break;
+    }
+    if (ballot(((l0 & E0) | (l1 & E1)) != 0u)) return -1;
+    uint32_t D0[4], D1[4], nw0 = 0, nw1 = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if ((am4 >> d) & 1u) {
+        const uint32_t x0 = F0[d], x1 = F1[d];
+        D0[d] = (x0 | (x0 << 1) | (x0 >> 1) | (x1 << 31) | from_prev_lane(x0) | from_next_lane(x0)) & A0;
+        D1[d] = (x1 | (x1 << 1) | (x1 >> 1) | (x0 >> 31) | from_prev_lane(x1) | from_next_lane(x1)) & A1;
+      } else {
+        D0[d] = D1[d] = 0u;
+      }
+      nw0 |= D0[d];
+      nw1 |= D1[d];
+    }
+    nw0 &= ~V0;
+    nw1 &= ~V1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 4; ++j) {
+        if (!((am4 >> i) & 1u) || !((am4 >> j) & 1u) || ((M >> (4 * i + j)) & 1u)) continue;
+        if (ballot(((D0[i] & (F0[j] | (D0[j] & nw0))) | (D1[i] & (F1[j] | (D1[j] & nw1)))) != 0u))
+          unite(i, j);
+      }
+    uint32_t reach = 0;  // directions with a new cell
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      F0[d] = D0[d] & nw0;
+      F1[d] = D1[d] & nw1;
+      reach |= ballot((F0[d] | F1[d]) != 0u) ? (1u << d) : 0u;
+    }
+    P0 = V0;
+    P1 = V1;
+    if (n_classes() == 1) {
+      verdict = 1;
+      break;
+    }
+    bool closed = false;  // a class none of whose directions reached a new cell
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      closed |= ((am4 >> d) & 1u) && (reach & (M >> (4 * d)) & 15u) == 0u;
+    if (closed) {
+      verdict = 0;
+      break;
+    }
+    V0 |= nw0;
+    V1 |= nw1;
+  }
+  // counters over the processed cells: degree = on-grid 4-neighbours
+  const uint32_t pc = (uint32_t)(__popc(P0) + __popc(P1));
+  uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
+  auto bit = [&](int pos) { return pos < 32 ? (P0 >> pos) & 1u : (P1 >> (pos - 32)) & 1u; };
+  if (c0 <= 0) dg -= bit(-c0);                // column 0 (window position -c0 <= 32)
+  if (W - c0 <= 64) dg -= bit(W - c0 - 1);    // column W - 1 (position >= 32)
+  bfs_nodes += wave_sum(pc);
+  bfs_deg += wave_sum(dg);
+  return verdict;
+}
+
 // Level-1 group sums of the one-chain-per-wave kernel: lane l owns groups l*PER .. l*PER +
 // PER-1 (PER even), stored as u16 pairs in dwords l*SD .. l*SD + PER/2 - 1, so a select
 // reads them with PER/2 dword loads.  The lane stride SD (PER/2, padded to the next odd
@@ -568,6 +696,7 @@ struct Ctx {
   GLB uint32_t* gscr;  // LB == 3, 5: this workgroup's 4-bit visit marks in HBM (all zero
                        // between searches; such labels cannot hold the search codes)
   int32_t qcap, k;
+  int32_t scap;  // race_search_g3: next-level entries staged over the group sums (<= 128)
   int lane;
   bool bb;  // grids: exact searches try the bitboard form first
   int my_dr, my_dc;
@@ -575,6 +704,7 @@ struct Ctx {
   uint32_t n_win = 0, n_bbs = 0, n_list = 0;  // contiguity checks by the path that decided
   uint64_t c_win = 0, c_bbs = 0, c_list = 0;  // s_memtime cycles spent in each path
   uint64_t n_bbl = 0;                          // bitboard levels run (decided or escaped)
+  uint64_t n_lvl = 0, c_atom = 0, c_clear = 0;  // race_search_g3: levels, claim / clear cycles
   __device__ static __forceinline__ uint64_t now() {
     uint64_t t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -998,6 +1128,169 @@ struct Ctx {
     return verdict == 1;
   }
 
+  // The race search of 3-bit-label grids (C5's 200x200 chains, whose exact searches at
+  // steady state run ~50 levels over ~1,000 cells): race_search_gscr's levels, pushes,
+  // merges and counters with three fewer HBM round trips per level.
+  //   - The marks of the four neighbours are read together; a claim of one found empty is
+  //     one atomic OR of the class's one-hot bit (m <= 4 on a grid) into its 4-bit field,
+  //     again four in flight.  The claimer that finds the field empty pushes the node; any other finds the bits of
+  //     classes that touched it before, all of them already merged with the owner by the
+  //     end of that level, so merging with the lowest one is the merge the list search
+  //     makes.  v is skipped by id instead of marked.
+  //   - A list entry carries its class (node | class << 16), so no mark is read back.
+  //   - The next level is staged in LDS over the chain's group sums (not read while the
+  //     search runs; up to scap entries, the displaced words held in two VGPRs); every
+  //     entry also goes to the HBM visit list (write-only until the marks are cleared),
+  //     from which a level larger than the stage is read.
+  __device__ __forceinline__ void gs_or_nr(int x, uint32_t bits) const {
+    __hip_atomic_fetch_or(gscr + (x >> 3), bits << ((x & 7) << 2), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ bool race_search_g3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
+                                 uint64_t& bfs_nodes, uint64_t& bfs_deg) {
+    LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
+    const uint32_t sv0 = lane < scap ? stage[lane] : 0u;
+    const uint32_t sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
+    lds_order();
+    if (lane < m) {
+      const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
+      gs_or_nr(src, 1u << lane);
+      spill[lane] = e;
+      stage[lane] = e;
+    }
+    __threadfence_block();  // the sources' marks precede every claim
+    int lb = 0, le = m;
+    uint32_t my_deg = 0;
+    uint64_t nodes = 0;
+    int verdict = -1;
+    for (;;) {
+      uint64_t rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
+      if (__popcll(rep) == 1) {
+        verdict = 1;
+        break;
+      }
+      const int cnt = le - lb;
+      const bool staged = cnt <= scap;
+      uint32_t q0 = 0u, q1 = 0u;
+      if (staged) {
+        if (lane < cnt) q0 = stage[lane];
+        if (lane + WAVE < cnt) q1 = stage[lane + WAVE];
+      }
+      lds_order();
+      uint64_t pushed_src = 0;
+      int nn = 0;
+      for (int cb = 0; cb < cnt; cb += WAVE) {
+        const int idx = cb + lane;
+        const bool act = idx < cnt;
+        uint32_t e = 0u;
+        if (staged)
+          e = cb == 0 ? q0 : q1;
+        else if (act)
+          e = spill[lb + idx];
+        const int x = (int)(e & 0xFFFFu);
+        const uint32_t o = e >> 16;
+        int xr = 0, xc = 0;
+        divmod(x, xr, xc);
+        if (act) my_deg += (uint32_t)degree(x, xr, xc);
+        nodes += (uint64_t)__popcll(ballot(act));
+        int y[4];
+        bool need[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          y[j] = act ? nbr(x, j, xr, xc) : -1;
+          need[j] = y[j] >= 0 && y[j] != v && L(y[j]) == a;
+        }
+#ifdef FW_STAMPS
+        const uint64_t t_at = now();
+#endif
+        // the marks are read first and only the cells found empty are claimed: an atomic on
+        // every a-labelled neighbour (most of them visited) measured 26% slower at C5's
+        // steady state (profiles/r03/g)
+        uint32_t got[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          got[j] = need[j] ? __hip_atomic_load(gscr + (y[j] >> 3), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (need[j] && ((got[j] >> ((y[j] & 7) << 2)) & 15u) == 0u)
+            got[j] = __hip_atomic_fetch_or(gscr + (y[j] >> 3), (1u << o) << ((y[j] & 7) << 2),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool pushed = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t nib = (got[j] >> ((y[j] & 7) << 2)) & 15u;
+          const bool push = need[j] && nib == 0u;
+          const bool req = need[j] && nib != 0u && ((nib >> o) & 1u) == 0u;
+          const uint64_t pm = ballot(push);
+          if (pm) {
+            if (push) {
+              const int slot = nn + (int)mbcnt(pm);
+              const uint32_t ent = (uint32_t)y[j] | (o << 16);
+              spill[le + slot] = ent;
+              if (slot < scap) stage[slot] = ent;
+            }
+            nn += __popcll(pm);
+          }
+          pushed |= push;
+          const uint32_t other = (uint32_t)__ffs(nib) - 1u;
+          uint64_t rm = ballot(req);
+          while (rm) {  // merges, serial over requesting lanes
+            const int Lr = __ffsll((unsigned long long)rm) - 1;
+            rm &= rm - 1;
+            const int o1 = rdl((int32_t)o, Lr), o2 = rdl((int32_t)other, Lr);
+            const uint64_t m1 = rdl64(cls, o1), m2 = rdl64(cls, o2);
+            if (m1 != m2) {
+              const uint64_t nm = m1 | m2;
+              if (lane < m && ((nm >> lane) & 1ull)) cls = nm;
+            }
+          }
+        }
+        for (int si = 0; si < m; ++si)
+          pushed_src |= ballot(pushed && o == (uint32_t)si) ? (1ull << si) : 0ull;
+#ifdef FW_STAMPS
+        c_atom += now() - t_at;
+#endif
+      }
+#ifdef FW_STAMPS
+      n_lvl += 1;
+#endif
+      lb = le;
+      le += nn;
+      if (nn > scap) __threadfence_block();  // the next level is read from the HBM list
+      lds_order();
+      rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
+      if (__popcll(rep) == 1) {
+        verdict = 1;
+        break;
+      }
+      // a class with no pushes this level is closed: disconnected
+      const bool closed = lane < m && ((rep >> lane) & 1ull) && ((cls & pushed_src) == 0ull);
+      if (ballot(closed)) {
+        verdict = 0;
+        break;
+      }
+    }
+    bfs_nodes += nodes;
+    bfs_deg += wave_sum(my_deg);
+#ifdef FW_STAMPS
+    const uint64_t t_cl = now();
+#endif
+    __threadfence_block();  // the visit list is read back
+    for (int base = 0; base < le; base += WAVE) {  // clear the marks
+      const int idx = base + lane;
+      if (idx < le) gs_clear((int)(spill[idx] & 0xFFFFu));
+    }
+    if (lane < scap) stage[lane] = sv0;
+    if (lane + WAVE < scap) stage[lane + WAVE] = sv1;
+    __threadfence_block();
+#ifdef FW_STAMPS
+    c_clear += now() - t_cl;
+#endif
+    return verdict == 1;
+  }
+
   // Exact verdict on "(district a) minus v is connected and non-empty", by a
   // level-synchronous race search from the m a-labelled neighbours of v (the
   // sources, in CSR order); cls holds, in lanes 0..m-1, the pre-merged class masks.
@@ -1185,10 +1478,13 @@ struct Ctx {
       if (bb) {  // bitboard search first; the list search past its window
         int vr, vc;
         divmod(v, vr, vc);
-        const int wv = grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a,
-                                        (uint32_t)(am >> 1) & 15u,
-                                        (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3)),
-                                        bfs_nodes, bfs_deg);
+        // 3-bit labels (large grids, C5): the 64-column window
+        const uint32_t am4 = (uint32_t)(am >> 1) & 15u;
+        const uint32_t lk = (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3));
+        const int wv = LB == 3 ? grid_race_bb2<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk,
+                                                   bfs_nodes, bfs_deg)
+                               : grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk,
+                                                  bfs_nodes, bfs_deg);
 #ifdef FW_STAMPS
         n_bbs += 1;
 #endif
@@ -1218,6 +1514,11 @@ struct Ctx {
       if (lane == i) src = val;
     }
     bool verdict;
+#ifndef FW_G3_OFF
+    if constexpr (LB == 3 && GRID)
+      verdict = race_search_g3(v, a, m, src, cls, scap, bfs_nodes, bfs_deg);
+    else
+#endif
     if constexpr (LB == 3 || LB == 5)
       verdict = race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else

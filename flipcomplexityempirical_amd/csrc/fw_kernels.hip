@@ -72,6 +72,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.gscr = LB == 3 || LB == 5 ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
   C.qcap = p.qcap;
+  C.scap = min(128, (p.off_list - p.off_gsum) / 4);
   C.k = p.k;
   C.bb = true;
   C.bb = !p.no_bb;
@@ -476,6 +477,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   CSTAMP_COUNT(11, C.c_win);
   CSTAMP_COUNT(12, C.c_bbs);
   CSTAMP_COUNT(13, C.c_list);
+  CSTAMP_COUNT(6, C.n_lvl);
+  CSTAMP_COUNT(7, C.c_atom);
+  CSTAMP_COUNT(14, C.c_clear);
 #endif
   CSTAMP_FLUSH
 }
@@ -492,6 +496,7 @@ __global__ __launch_bounds__(64) void fw_eval_kernel(FwEvalParams p) {
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.qcap = p.qcap;
+  C.scap = 0;  // 4- and 8-bit labels only: race_search_g3 is not instantiated
   C.k = p.k;
   C.bb = true;
   C.init_roles();

@@ -25,11 +25,14 @@ static int W, H;
 typedef struct {
   long n;
   double levels, nodes, bglevels, bgnodes, minlevels;
-  long connected, fit6432, fit6464, fit12864, fit128, bgwins;
+  long connected, fit6432, fit6464, fit12864, fit128, fit6496, fit64128, bgwins;
   double esc_levels, esc_nodes;
   long hist[8];  /* levels of min(A, background) in bins <4, <8, <16, <32, <64, <128, <256, >= */
   long histA[8];
 } acc_t;
+
+static long g_fr_hist[6]; /* max frontier (next level) per search: <=64, <=128, <=256, <=512, <=1024, more */
+static int g_fr_max;
 
 static int lvl_bin(int l) {
   int b = 0, t = 4;
@@ -52,6 +55,7 @@ static int race_a(chain_t* c, int32_t v, int16_t a, const int32_t* src, int32_t 
   int verdict = -1;
   *levels = 0;
   *nodes = 0;
+  g_fr_max = 0;
   for (;;) {
     int32_t ncls = 0;
     for (int32_t i = 0; i < m; ++i) ncls += uf_find(uf, i) == i;
@@ -77,6 +81,7 @@ static int race_a(chain_t* c, int32_t v, int16_t a, const int32_t* src, int32_t 
     }
     lb = le;
     le = nl;
+    if (le - lb > g_fr_max) g_fr_max = le - lb;
     ncls = 0;
     for (int32_t i = 0; i < m; ++i) ncls += uf_find(uf, i) == i;
     if (ncls == 1) { verdict = 1; break; }
@@ -88,6 +93,11 @@ static int race_a(chain_t* c, int32_t v, int16_t a, const int32_t* src, int32_t 
     if (ex) { verdict = 0; break; }
   }
   for (int32_t li = 0; li < nl; ++li) c->owner[c->list[li]] = -1;
+  {
+    int b = 0, t = 64;
+    while (b < 5 && g_fr_max > t) { ++b; t *= 2; }
+    g_fr_hist[b]++;
+  }
   return verdict;
 }
 
@@ -293,6 +303,8 @@ int main(int argc, char** argv) {
         A.fit6464 += mdr < 32 && mdc < 32;
         A.fit128 += mdr < 64 && mdc < 64;
         A.fit12864 += mdr < 64 && mdc < 32;
+        A.fit6496 += mdr < 32 && mdc < 48;
+        A.fit64128 += mdr < 32 && mdc < 64;
         if (!(mdr < 32 && mdc < 16)) { A.esc_levels += lv; A.esc_nodes += nd; }
         A.hist[lvl_bin(lv < blv ? lv : blv)]++;
         A.histA[lvl_bin(lv)]++;
@@ -319,6 +331,12 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 8; ++i) printf(" %.3f", (double)A.histA[i] / A.n);
     printf("\n  levels min   <4 <8 <16 <32 <64 <128 <256 >=:");
     for (int i = 0; i < 8; ++i) printf(" %.3f", (double)A.hist[i] / A.n);
+    printf("\n  fits 64 rows x 96 cols %.3f, 64 x 128 %.3f", (double)A.fit6496 / A.n,
+           (double)A.fit64128 / A.n);
+    printf("\n  max frontier <=64 <=128 <=256 <=512 <=1024 more:");
+    long fr_n = 0;
+    for (int i = 0; i < 6; ++i) fr_n += g_fr_hist[i];
+    for (int i = 0; i < 6; ++i) printf(" %.4f", (double)g_fr_hist[i] / (fr_n ? fr_n : 1));
     printf("\n");
   }
   return 0;

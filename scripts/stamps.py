@@ -4,7 +4,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["FLIPWALK_LIB"] = os.path.join(ROOT, "flipcomplexityempirical_amd", "libflipwalk_stamps.so")
+os.environ.setdefault("FLIPWALK_LIB", os.path.join(ROOT, "flipcomplexityempirical_amd", "libflipwalk_stamps.so"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
@@ -14,7 +14,8 @@ from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bo
 L = _lib.load()
 L.fw_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 # usage: stamps.py [config] [chains] [warm launches]   (config c3 default; c5 = the 64-base
-# ladder workload; warm launches of 1000 steps before the stamped ones, default 2)
+# ladder workload; warm launches of 1000 steps before the stamped ones, default 2; an
+# optional checkpoint to resume from first)
 from flipcomplexityempirical_amd.workloads import workload  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 w = workload(cfg)
@@ -23,6 +24,12 @@ g = w.graph
 dg = DeviceGraph(g)
 ch = Chains(dg, nch, w.k, w.init, proposal=w.proposal,
             pop_bounds=population_bounds(g.total_pop, w.k, w.percent), base=w.bases(0, nch), seed=0)
+if len(sys.argv) > 4:  # a bench.py --save-checkpoint file of the same workload and chains
+    from flipcomplexityempirical_amd.chain import STATS_DTYPE  # noqa: E402
+    ckf = np.load(sys.argv[4], allow_pickle=False)
+    ck = {key: ckf[key] for key in ckf.files}
+    ck["stats"] = ckf["stats"].view(STATS_DTYPE)
+    ch.restore(ck)
 for _ in range(int(sys.argv[3]) if len(sys.argv) > 3 else 2):
     ch.run(1000)
 buf = np.zeros(16, np.uint64)
@@ -57,6 +64,10 @@ if cb[:6].sum():
         print(f"{nm:18s} {v / tot * 100:6.2f} %  {v / att:8.1f} clk/attempt")
     print(f"contiguity decided by: 7x7 window {cb[8] / att:.3f}/attempt, bitboard search "
           f"{cb[9] / att:.3f}, list search {cb[10] / att:.3f}")
+    if cb[6]:
+        print(f"list search (race_search_g3): {cb[6] / max(cb[10], 1):.1f} levels per run, "
+              f"claim+merge {cb[7] / cb[6]:.0f} clk per level, clearing {cb[14] / max(cb[10], 1):.0f} "
+              f"clk per run")
     if cb[11] + cb[12] + cb[13]:
         print(f"contiguity cycles by path (per attempt / per run): 7x7 window "
               f"{cb[11] / att:.0f} / {cb[11] / max(cb[8], 1):.0f}, bitboard {cb[12] / att:.0f} / "

@@ -257,6 +257,43 @@ def test_large_grid_ladder_bit_exact(gpu_lib, n, k, bw, variant, monkeypatch):
         assert_stats_equal(st[i:i + 1], ost)
 
 
+@pytest.mark.parametrize("variant", ["auto", "list"])
+def test_large_grid_deep_search_bit_exact(gpu_lib, variant, monkeypatch):
+    """C5 past burn-in: 200x200, k=8, low ladder bases (0.1 .. 1) for 40,000 steps, where
+    the districts are fractal (cut ~ 30% of the edges) and the exact searches that leave the
+    7x7 window run tens of levels over hundreds of cells (scripts/search_stats.c): the
+    HBM-marked search (race_search_g3: one-hot claims, LDS-staged levels, levels larger
+    than the stage read from the HBM list) against the oracle, bit for bit.  list: every
+    exact search as that list search."""
+    from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
+    from flipcomplexityempirical_amd.graph import block_seed, grid_graph
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    if variant == "list":
+        monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
+    n, k = 200, 8
+    g = grid_graph(n, n)
+    init = block_seed(n, n, 2, 4)
+    bounds = population_bounds(g.total_pop, k, 0.05)
+    bases = np.array([0.1, 0.25, 0.5, 1.0])
+    steps = (20000, 20000)
+    dg = DeviceGraph(g)
+    ch = Chains(dg, len(bases), k, init, proposal="pairs", pop_bounds=bounds, base=bases,
+                seed=11, chain_id0=77)
+    for s in steps:
+        ch.run(s)
+    labs, st = ch.labels(), ch.stats()
+    assert st["bfs_nodes"].sum() > 20 * st["bfs_runs"].sum() > 0
+    for i, b in enumerate(bases):
+        lab, ost = init.copy(), O.new_stats(1)
+        for s in steps:
+            lab, ost, _, _ = O.run_chain(g, lab, k, 1, *bounds, metropolis_table(b, 4), 11,
+                                         77 + i, s, stats=ost)
+        assert np.array_equal(labs[i], lab), i
+        assert_stats_equal(st[i:i + 1], ost)
+    ch.close()
+    dg.close()
+
+
 def _ramp(t):
     """A short stand-in for the reference's commented beta ramp (grid_chain_sec11.py:88-93)."""
     if t < 40:
