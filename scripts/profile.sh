@@ -11,7 +11,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 bench.py $BENCH_ARGS > $OUT/ktrace_bench.log 2>&1 || { echo "ktrace failed rc=$?"; tail -20 $OUT/ktrace_bench.log; exit 1; }
 tail -1 $OUT/ktrace_bench.log
-PB="--steps 1 --warmup 1 --inner 1000 --no-cpu-baseline $CFG_ARGS"
+PB=${PMC_ARGS:-"--steps 1 --warmup 1 --inner 1000 --no-cpu-baseline --check-chains 0 $CFG_ARGS"}
 i=0
 for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
             "SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_BRANCH" \
