@@ -1706,8 +1706,8 @@ void* fw_grid16_fn(const FwRunParams& p) {
 // grid16_body) and the waves per workgroup (1..4) that maximise a throughput model: chains
 // in flight (resident waves x 4/R, at most the chains there are) x the attempts a chain
 // consumes per wave iteration, E(R) = 1 + q + ... + q^(R-1) with q = 0.56 the probability
-// that an attempt leaves the state unchanged (C3), x 0.9 for R > 1 (its 128-VGPR budget and
-// the merge).  Ties: R = 1, then fewer waves.  FLIPWALK_SPEC=1/2/4 forces R.
+// that an attempt leaves the state unchanged (C3), x the measured per-row speed of the R > 1
+// kernels.  Ties: R = 1, then fewer waves.  FLIPWALK_SPEC=1/2/4 forces R.
 int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   // slot: labels | u16 group sums (16 x PER per row; BIG: padded to whole supergroups) |
   // BIG: u16 supergroup sums (16 x PER)
@@ -1756,7 +1756,10 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
     }
     if (r_nw == 0) continue;
     const double e_r = R == 1 ? 1.0 : (R == 2 ? 1.56 : 1.0 + 0.56 + 0.56 * 0.56 + 0.56 * 0.56 * 0.56);
-    const double eff = R == 1 ? 1.0 : 0.9;
+    // per-row speed of the speculative kernels relative to R = 1 (their 128-VGPR budget
+    // spills ~60 VGPRs; the merge), calibrated on profiles/r03/e/ab_spec.jsonl: C2 (4,096
+    // chains) R = 4 +5..8% over R = 1, the 8,192-chain C3 shard R = 2 -1..-2.5%
+    const double eff = R == 1 ? 1.0 : (R == 2 ? 0.6 : 0.52);
     const double waves = (double)r_blocks * r_nw * prop.multiProcessorCount;
     const double units = (double)((p.n_chains + cpw - 1) / cpw);
     const double score = std::min(units, waves) * cpw * e_r * eff;
