@@ -704,7 +704,8 @@ struct Ctx {
   uint32_t n_win = 0, n_bbs = 0, n_list = 0;  // contiguity checks by the path that decided
   uint64_t c_win = 0, c_bbs = 0, c_list = 0;  // s_memtime cycles spent in each path
   uint64_t n_bbl = 0;                          // bitboard levels run (decided or escaped)
-  uint64_t n_lvl = 0, c_atom = 0, c_clear = 0;  // race_search_g3: levels, claim / clear cycles
+  uint64_t n_lvl = 0, c_atom = 0, c_clear = 0;  // list searches: levels, claim / clear cycles
+  uint64_t n_mapt = 0;                           // race_search_b3: rounds of map tests
   __device__ static __forceinline__ uint64_t now() {
     uint64_t t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1291,6 +1292,236 @@ struct Ctx {
     return verdict == 1;
   }
 
+  // The race search of 3-bit-label grids with its visit marks in the labels themselves:
+  // the same levels, pushes, merges and counters as race_search_gscr (the oracle's
+  // contiguous_after), with LDS round trips where that search pays HBM ones.  A claimed
+  // node's label a becomes its class's code c_o; codes are the unused labels k..7 first,
+  // then borrowed district labels.  A borrowed code is ambiguous (a node of that district,
+  // or a visited one), so claims under it also set the node's bit in a 1-bit-per-node HBM
+  // map (agent-scope atomics; n/32 words per workgroup, L2-resident), read only when a
+  // frontier node of another, unmerged class meets the code: the merge test.  Within a
+  // level the four neighbour directions run one after another, so a node claimed in an
+  // earlier direction reads as claimed (LDS ops of one wave execute in program order) and
+  // no node is pushed twice: on a grid, two frontier nodes reach the same node in one
+  // direction only if they are the same node.  The ambiguous merge tests of a chunk are
+  // resolved together after it (merges are unions: their order within a level does not
+  // change the classes at its end).  Labels and map bits are restored from the HBM visit
+  // list at the end; levels are staged in LDS over the group sums as in race_search_g3.
+  __device__ bool race_search_b3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
+                                 uint64_t& bfs_nodes, uint64_t& bfs_deg) {
+    LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
+    GLB uint32_t* const bm = gscr;  // 1 bit per node
+    // class codes: unused labels first, then borrowed ones, preferring district labels
+    // absent from a sample of 256 cells around v (a 16 x 16 lattice of step 4): a code
+    // met by a frontier is then rarely a real district cell, so map tests stay rare
+    uint32_t codes = 0, ambig = 0;  // 3-bit code of class o at bits 3o; ambiguous: bit o
+    {
+      int vr, vc;
+      divmod(v, vr, vc);
+      uint32_t seen = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int cell = lane + WAVE * t;  // 0..255
+        const int rr = vr + 4 * (cell >> 4) - 30, cc = vc + 4 * (cell & 15) - 30;
+        if (rr >= 0 && rr < g.gh && cc >= 0 && cc < g.gw) seen |= 1u << L(rr * g.gw + cc);
+      }
+      seen = (uint32_t)wave_or64(seen);
+      int o = 0;
+      for (uint32_t c = (uint32_t)k; c < 8u && o < m; ++c, ++o) codes |= c << (3 * o);
+      for (int pass = 0; pass < 2; ++pass)  // absent labels first, then present ones
+        for (uint32_t t = 1; t < 8u && o < m; ++t) {
+          const uint32_t c = (a + t) & 7u;
+          if (c >= (uint32_t)k || ((seen >> c) & 1u) != (uint32_t)pass) continue;
+          codes |= c << (3 * o);
+          ambig |= 1u << o;
+          ++o;
+        }
+    }
+    // code -> class + 1 (0: not a class code), 8 entries of 3 bits
+    uint32_t cls_of = 0;
+    for (int o = 0; o < m; ++o) cls_of |= (uint32_t)(o + 1) << (3 * ((codes >> (3 * o)) & 7u));
+    // classes as 4-bit member masks of the sources (uniform), from the pre-merged cls
+    uint32_t M = 0;
+    for (int i = 0; i < m; ++i) M |= ((uint32_t)rdl64(cls, i) & 15u) << (4 * i);
+    auto unite = [&](int i, int j) {
+      const uint32_t mm = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        if ((mm >> d) & 1u) M = (M & ~(15u << (4 * d))) | (mm << (4 * d));
+    };
+    auto n_classes = [&]() {
+      int nc = 0;
+      for (int i = 0; i < m; ++i) nc += (__ffs((M >> (4 * i)) & 15u) - 1) == i;
+      return nc;
+    };
+    const uint32_t sv0 = lane < scap ? stage[lane] : 0u;
+    const uint32_t sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
+    lds_order();
+    if (lane < m) {
+      const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
+      P::axor(lab, src, a ^ ((codes >> (3 * lane)) & 7u));
+      if ((ambig >> lane) & 1u)
+        __hip_atomic_fetch_or(bm + (src >> 5), 1u << (src & 31), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      spill[lane] = e;
+      stage[lane] = e;
+    }
+    lds_order();
+    int lb = 0, le = m;
+    uint32_t my_deg = 0;
+    uint64_t nodes = 0;
+    int verdict = -1;
+    for (;;) {
+      if (n_classes() == 1) {
+        verdict = 1;
+        break;
+      }
+      const int cnt = le - lb;
+      const bool staged = cnt <= scap;
+      uint32_t q0 = 0u, q1 = 0u;
+      if (staged) {
+        if (lane < cnt) q0 = stage[lane];
+        if (lane + WAVE < cnt) q1 = stage[lane + WAVE];
+      }
+      lds_order();
+      uint32_t pushed_src = 0;
+      int nn = 0;
+      for (int cb = 0; cb < cnt; cb += WAVE) {
+        const int idx = cb + lane;
+        const bool act = idx < cnt;
+        uint32_t e = 0u;
+        if (staged)
+          e = cb == 0 ? q0 : q1;
+        else if (act)
+          e = spill[lb + idx];
+        const int x = (int)(e & 0xFFFFu);
+        const uint32_t o = e >> 16;
+        const uint32_t co = (codes >> (3 * o)) & 7u;
+        const bool amb_o = (ambig >> o) & 1u;
+        int xr = 0, xc = 0;
+        divmod(x, xr, xc);
+        if (act) my_deg += (uint32_t)degree(x, xr, xc);
+        nodes += (uint64_t)__popcll(ballot(act));
+        bool pushed = false;
+        uint32_t chk = 0;   // ambiguous merge tests: bit j
+        uint32_t chk_o = 0; // their classes, 3 bits per j
+        int ys[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int y = act ? nbr(x, j, xr, xc) : -1;
+          ys[j] = y;
+          const bool ok = y >= 0 && y != v;
+          const uint32_t ly = L(ok ? y : x);
+          const bool push = ok && ly == a;
+          if (push) P::axor(lab, y, a ^ co);
+          const uint64_t pm = ballot(push);
+          if (pm) {
+            if (push) {
+              if (amb_o)
+                __hip_atomic_fetch_or(bm + (y >> 5), 1u << (y & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+              const int slot = nn + (int)mbcnt(pm);
+              const uint32_t ent = (uint32_t)y | (o << 16);
+              spill[le + slot] = ent;
+              if (slot < scap) stage[slot] = ent;
+            }
+            nn += __popcll(pm);
+          }
+          pushed |= push;
+          // a class code of another class not yet merged with this one: a merge if the
+          // node is a visited one (certain for unused-label codes, a map test otherwise)
+          const uint32_t c1 = ok && !push ? (cls_of >> (3 * ly)) & 7u : 0u;
+          const bool other = c1 != 0u && ((M >> (4 * o + (c1 - 1u))) & 1u) == 0u;
+          const bool sure = other && !((ambig >> (c1 - 1u)) & 1u);
+          if (other && !sure) {
+            chk |= 1u << j;
+            chk_o |= (c1 - 1u) << (3 * j);
+          }
+          uint64_t rm = ballot(sure);
+          while (rm) {  // merges, serial over requesting lanes
+            const int Lr = __ffsll((unsigned long long)rm) - 1;
+            rm &= rm - 1;
+            unite(rdl((int32_t)o, Lr), rdl((int32_t)(c1 - 1u), Lr));
+          }
+        }
+        if (ballot(chk != 0u)) {  // the map tests of this chunk, after its claims landed
+#ifdef FW_STAMPS
+          n_mapt += 1;
+#endif
+          __threadfence_block();
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            w[j] = ((chk >> j) & 1u) ? __hip_atomic_load(bm + (ys[j] >> 5), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool hit = ((chk >> j) & 1u) && ((w[j] >> (ys[j] & 31)) & 1u);
+            uint64_t rm = ballot(hit);
+            while (rm) {
+              const int Lr = __ffsll((unsigned long long)rm) - 1;
+              rm &= rm - 1;
+              unite(rdl((int32_t)o, Lr), rdl((int32_t)((chk_o >> (3 * j)) & 7u), Lr));
+            }
+          }
+        }
+        for (int si = 0; si < m; ++si)
+          pushed_src |= ballot(pushed && o == (uint32_t)si) ? (1u << si) : 0u;
+      }
+#ifdef FW_STAMPS
+      n_lvl += 1;
+#endif
+      lb = le;
+      le += nn;
+      if (nn > scap) __threadfence_block();  // the next level is read from the HBM list
+      lds_order();
+      if (n_classes() == 1) {
+        verdict = 1;
+        break;
+      }
+      // a class none of whose sources pushed this level is closed: disconnected
+      bool closed = false;
+      for (int i = 0; i < m; ++i)
+        closed |= (__ffs((M >> (4 * i)) & 15u) - 1) == i && ((M >> (4 * i)) & pushed_src & 15u) == 0u;
+      if (closed) {
+        verdict = 0;
+        break;
+      }
+    }
+    bfs_nodes += nodes;
+    bfs_deg += wave_sum(my_deg);
+#ifdef FW_STAMPS
+    const uint64_t t_cl = now();
+#endif
+    __threadfence_block();  // the visit list is read back
+    // restore the labels, clear the map bits: eight list loads per lane in flight at a time
+    for (int base = 0; base < le; base += 8 * WAVE) {
+      uint32_t ev[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * WAVE + lane;
+        ev[u] = idx < le ? spill[idx] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (ev[u] == 0xFFFFFFFFu) continue;
+        const int x = (int)(ev[u] & 0xFFFFu);
+        const uint32_t o = ev[u] >> 16;
+        P::axor(lab, x, a ^ ((codes >> (3 * o)) & 7u));
+        if ((ambig >> o) & 1u)
+          __hip_atomic_fetch_and(bm + (x >> 5), ~(1u << (x & 31)), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (lane < scap) stage[lane] = sv0;
+    if (lane + WAVE < scap) stage[lane + WAVE] = sv1;
+    __threadfence_block();
+#ifdef FW_STAMPS
+    c_clear += now() - t_cl;
+#endif
+    return verdict == 1;
+  }
+
   // Exact verdict on "(district a) minus v is connected and non-empty", by a
   // level-synchronous race search from the m a-labelled neighbours of v (the
   // sources, in CSR order); cls holds, in lanes 0..m-1, the pre-merged class masks.
@@ -1516,7 +1747,11 @@ struct Ctx {
     bool verdict;
 #ifndef FW_G3_OFF
     if constexpr (LB == 3 && GRID)
+#ifdef FW_G3
       verdict = race_search_g3(v, a, m, src, cls, scap, bfs_nodes, bfs_deg);
+#else
+      verdict = race_search_b3(v, a, m, src, cls, scap, bfs_nodes, bfs_deg);
+#endif
     else
 #endif
     if constexpr (LB == 3 || LB == 5)

@@ -480,6 +480,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   CSTAMP_COUNT(6, C.n_lvl);
   CSTAMP_COUNT(7, C.c_atom);
   CSTAMP_COUNT(14, C.c_clear);
+  CSTAMP_COUNT(15, C.n_mapt);
 #endif
   CSTAMP_FLUSH
 }
