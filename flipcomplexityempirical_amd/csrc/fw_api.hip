@@ -664,7 +664,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   }
   p.seg_done = c->d_segdone;
   if ((lb == 3 || lb == 5) && !use16) {  // HBM visit marks of the chain kernel's list search
-    p.gscr_words = (n + 7) / 8;
+    // 4-bit marks of race_search_gscr; 3-bit grids: race_search_b3's byte map
+    p.gscr_words = lb == 3 && g->gw > 0 ? (n + 3) / 4 : (n + 7) / 8;
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
     if (hipMalloc(&c->d_gscr, gb) != hipSuccess || hipMemset(c->d_gscr, 0, gb) != hipSuccess) {
       fw_chains_destroy(c);

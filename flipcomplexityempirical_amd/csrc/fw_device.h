@@ -1297,9 +1297,9 @@ struct Ctx {
   // contiguous_after), with LDS round trips where that search pays HBM ones.  A claimed
   // node's label a becomes its class's code c_o; codes are the unused labels k..7 first,
   // then borrowed district labels.  A borrowed code is ambiguous (a node of that district,
-  // or a visited one), so claims under it also set the node's bit in a 1-bit-per-node HBM
-  // map (agent-scope atomics; n/32 words per workgroup, L2-resident), read only when a
-  // frontier node of another, unmerged class meets the code: the merge test.  Within a
+  // or a visited one), so claims under it also set the node's byte in an HBM map (n bytes
+  // per workgroup), read only when a frontier node of another, unmerged class meets the
+  // code: the merge test.  Within a
   // level the four neighbour directions run one after another, so a node claimed in an
   // earlier direction reads as claimed (LDS ops of one wave execute in program order) and
   // no node is pushed twice: on a grid, two frontier nodes reach the same node in one
@@ -1310,7 +1310,11 @@ struct Ctx {
   __device__ bool race_search_b3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
                                  uint64_t& bfs_nodes, uint64_t& bfs_deg) {
     LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
-    GLB uint32_t* const bm = gscr;  // 1 bit per node
+    // the map: one byte per node, set and cleared by plain byte stores (global atomics
+    // execute past the XCD's L2 and drop the line), read by L2-served sc1 loads after the
+    // stores have drained
+    GLB uint32_t* const bm = gscr;
+    GLB uint8_t* const bmap = reinterpret_cast<GLB uint8_t*>(gscr);
     // class codes: unused labels first, then borrowed ones, preferring district labels
     // absent from a sample of 256 cells around v (a 16 x 16 lattice of step 4): a code
     // met by a frontier is then rarely a real district cell, so map tests stay rare
@@ -1360,9 +1364,7 @@ struct Ctx {
     if (lane < m) {
       const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
       P::axor(lab, src, a ^ ((codes >> (3 * lane)) & 7u));
-      if ((ambig >> lane) & 1u)
-        __hip_atomic_fetch_or(bm + (src >> 5), 1u << (src & 31), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
+      if ((ambig >> lane) & 1u) bmap[src] = 1u;
       spill[lane] = e;
       stage[lane] = e;
     }
@@ -1417,9 +1419,7 @@ struct Ctx {
           const uint64_t pm = ballot(push);
           if (pm) {
             if (push) {
-              if (amb_o)
-                __hip_atomic_fetch_or(bm + (y >> 5), 1u << (y & 31), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+              if (amb_o) bmap[y] = 1u;
               const int slot = nn + (int)mbcnt(pm);
               const uint32_t ent = (uint32_t)y | (o << 16);
               spill[le + slot] = ent;
@@ -1452,11 +1452,11 @@ struct Ctx {
           uint32_t w[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            w[j] = ((chk >> j) & 1u) ? __hip_atomic_load(bm + (ys[j] >> 5), __ATOMIC_RELAXED,
+            w[j] = ((chk >> j) & 1u) ? __hip_atomic_load(bm + (ys[j] >> 2), __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const bool hit = ((chk >> j) & 1u) && ((w[j] >> (ys[j] & 31)) & 1u);
+            const bool hit = ((chk >> j) & 1u) && ((w[j] >> ((ys[j] & 3) << 3)) & 0xFFu);
             uint64_t rm = ballot(hit);
             while (rm) {
               const int Lr = __ffsll((unsigned long long)rm) - 1;
@@ -1494,23 +1494,14 @@ struct Ctx {
     const uint64_t t_cl = now();
 #endif
     __threadfence_block();  // the visit list is read back
-    // restore the labels, clear the map bits: eight list loads per lane in flight at a time
-    for (int base = 0; base < le; base += 8 * WAVE) {
-      uint32_t ev[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int idx = base + u * WAVE + lane;
-        ev[u] = idx < le ? spill[idx] : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (ev[u] == 0xFFFFFFFFu) continue;
-        const int x = (int)(ev[u] & 0xFFFFu);
-        const uint32_t o = ev[u] >> 16;
+    for (int base = 0; base < le; base += WAVE) {  // restore the labels, clear the map
+      const int idx = base + lane;
+      if (idx < le) {
+        const uint32_t e = spill[idx];
+        const int x = (int)(e & 0xFFFFu);
+        const uint32_t o = e >> 16;
         P::axor(lab, x, a ^ ((codes >> (3 * o)) & 7u));
-        if ((ambig >> o) & 1u)
-          __hip_atomic_fetch_and(bm + (x >> 5), ~(1u << (x & 31)), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+        if ((ambig >> o) & 1u) bmap[x] = 0u;
       }
     }
     if (lane < scap) stage[lane] = sv0;
