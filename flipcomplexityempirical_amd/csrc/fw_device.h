@@ -574,14 +574,12 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
   E0 &= A0;
   E1 &= A1;
   // frontier per direction; sources up (31, 32), left (32, 31), right (32, 33), down (33, 32)
-  uint32_t F0[4], F1[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
+  auto src_bits = [lane](int d, uint32_t& b0, uint32_t& b1) {
     const int sl = d == 0 ? 31 : (d == 3 ? 33 : 32);
-    const bool on = lane == sl && ((am4 >> d) & 1u);
-    F0[d] = on && d == 1 ? 0x80000000u : 0u;
-    F1[d] = on && d != 1 ? (d == 2 ? 2u : 1u) : 0u;
-  }
+    const bool on = lane == sl;
+    b0 = on && d == 1 ? 0x80000000u : 0u;
+    b1 = on && d != 1 ? (d == 2 ? 2u : 1u) : 0u;
+  };
   uint32_t M = 0x8421u;  // class of direction d: 4-bit member mask at bits 4d (uniform)
   auto unite = [&](int i, int j) {
     const uint32_t m = ((M >> (4 * i)) | (M >> (4 * j))) & 15u;
@@ -600,6 +598,67 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
       nc += (int)(((am4 >> d) & 1u) && (__ffs((M >> (4 * d)) & 15u) - 1) == d);
     return nc;
   };
+  if (n_classes() == 2) {
+    // two classes after the ring links (91% of C5's exact searches at steady state): one
+    // frontier per class (the union of its directions' frontiers: dilation and the merge
+    // test distribute over unions, and a class is closed when every direction of it is),
+    // one merge test per level; the general loop's levels, stopping rules and counters
+    uint32_t Fa0 = 0u, Fa1 = 0u, Fb0 = 0u, Fb1 = 0u;
+    int ra = -1;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!((am4 >> d) & 1u)) continue;
+      uint32_t b0, b1;
+      src_bits(d, b0, b1);
+      const int rep = __ffs((M >> (4 * d)) & 15u) - 1;
+      if (ra < 0) ra = rep;
+      if (rep == ra) {
+        Fa0 |= b0;
+        Fa1 |= b1;
+      } else {
+        Fb0 |= b0;
+        Fb1 |= b1;
+      }
+    }
+    uint32_t V0 = Fa0 | Fb0, V1 = Fa1 | Fb1;
+    int vd;
+    for (;;) {
+      if (ballot((((Fa0 | Fb0) & E0) | ((Fa1 | Fb1) & E1)) != 0u)) return -1;
+      const uint32_t Da0 = (Fa0 | (Fa0 << 1) | (Fa0 >> 1) | (Fa1 << 31) | from_prev_lane(Fa0) | from_next_lane(Fa0)) & A0;
+      const uint32_t Da1 = (Fa1 | (Fa1 << 1) | (Fa1 >> 1) | (Fa0 >> 31) | from_prev_lane(Fa1) | from_next_lane(Fa1)) & A1;
+      const uint32_t Db0 = (Fb0 | (Fb0 << 1) | (Fb0 >> 1) | (Fb1 << 31) | from_prev_lane(Fb0) | from_next_lane(Fb0)) & A0;
+      const uint32_t Db1 = (Fb1 | (Fb1 << 1) | (Fb1 >> 1) | (Fb0 >> 31) | from_prev_lane(Fb1) | from_next_lane(Fb1)) & A1;
+      const uint32_t nw0 = (Da0 | Db0) & ~V0, nw1 = (Da1 | Db1) & ~V1;
+      if (ballot(((Da0 & (Fb0 | (Db0 & nw0))) | (Da1 & (Fb1 | (Db1 & nw1)))) != 0u)) {
+        vd = 1;  // the two classes met: connected, the cells processed are V
+        break;
+      }
+      Fa0 = Da0 & nw0;
+      Fa1 = Da1 & nw1;
+      Fb0 = Db0 & nw0;
+      Fb1 = Db1 & nw1;
+      if (!ballot((Fa0 | Fa1) != 0u) || !ballot((Fb0 | Fb1) != 0u)) {
+        vd = 0;  // a class reached no new cell: closed, disconnected
+        break;
+      }
+      V0 |= nw0;
+      V1 |= nw1;
+    }
+    const uint32_t pc = (uint32_t)(__popc(V0) + __popc(V1));
+    uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
+    auto vbit = [&](int pos) { return pos < 32 ? (V0 >> pos) & 1u : (V1 >> (pos - 32)) & 1u; };
+    if (c0 <= 0) dg -= vbit(-c0);
+    if (W - c0 <= 64) dg -= vbit(W - c0 - 1);
+    bfs_nodes += wave_sum(pc);
+    bfs_deg += wave_sum(dg);
+    return vd;
+  }
+  uint32_t F0[4], F1[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    src_bits(d, F0[d], F1[d]);
+    if (!((am4 >> d) & 1u)) F0[d] = F1[d] = 0u;
+  }
   uint32_t V0 = F0[0] | F0[1] | F0[2] | F0[3], V1 = F1[0] | F1[1] | F1[2] | F1[3];
   int verdict = -1;
   uint32_t P0, P1;  // processed cells

@@ -33,6 +33,7 @@ typedef struct {
 
 static long g_fr_hist[6]; /* max frontier (next level) per search: <=64, <=128, <=256, <=512, <=1024, more */
 static int g_fr_max;
+static long g_mcls[5][5]; /* exact searches by sources m and classes after the ring links */
 
 static int lvl_bin(int l) {
   int b = 0, t = 4;
@@ -284,6 +285,11 @@ int main(int argc, char** argv) {
       else {
         int lv, mdr, mdc, blv, mp;
         long nd, bnd;
+        {
+          int ncls = 0;
+          for (int32_t i = 0; i < m; ++i) ncls += uf_find(uf, i) == i;
+          g_mcls[m < 5 ? m : 4][ncls < 5 ? ncls : 4]++;
+        }
         int va = race_a(&c, v, a, src, m, uf, &lv, &nd, &mdr, &mdc);
         int vb = race_bg(&c, v, a, &blv, &bnd, &mp);
         if (va != vb) {
@@ -333,6 +339,10 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 8; ++i) printf(" %.3f", (double)A.hist[i] / A.n);
     printf("\n  fits 64 rows x 96 cols %.3f, 64 x 128 %.3f", (double)A.fit6496 / A.n,
            (double)A.fit64128 / A.n);
+    printf("\n  exact searches by (sources, classes):");
+    for (int i = 2; i < 5; ++i)
+      for (int j = 1; j < 5; ++j)
+        if (g_mcls[i][j]) printf(" (%d,%d) %.3f", i, j, (double)g_mcls[i][j] / A.n);
     printf("\n  max frontier <=64 <=128 <=256 <=512 <=1024 more:");
     long fr_n = 0;
     for (int i = 0; i < 6; ++i) fr_n += g_fr_hist[i];

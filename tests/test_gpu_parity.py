@@ -257,20 +257,21 @@ def test_large_grid_ladder_bit_exact(gpu_lib, n, k, bw, variant, monkeypatch):
         assert_stats_equal(st[i:i + 1], ost)
 
 
-@pytest.mark.parametrize("variant", ["auto", "list"])
-def test_large_grid_deep_search_bit_exact(gpu_lib, variant, monkeypatch):
-    """C5 past burn-in: 200x200, k=8, low ladder bases (0.1 .. 1) for 40,000 steps, where
-    the districts are fractal (cut ~ 30% of the edges) and the exact searches that leave the
-    7x7 window run tens of levels over hundreds of cells (scripts/search_stats.c): the
-    HBM-marked search (race_search_g3: one-hot claims, LDS-staged levels, levels larger
-    than the stage read from the HBM list) against the oracle, bit for bit.  list: every
-    exact search as that list search."""
+@pytest.mark.parametrize("n,variant", [(200, "auto"), (200, "list"), (160, "list")])
+def test_large_grid_deep_search_bit_exact(gpu_lib, n, variant, monkeypatch):
+    """C5 past burn-in: n x n, k=8, low ladder bases (0.1 .. 1) for 40,000 steps, where the
+    districts are fractal (cut ~ 30% of the edges) and the exact searches that leave the
+    7x7 window run tens of levels over hundreds of cells (scripts/search_stats.c), against
+    the oracle bit for bit.  auto: the 64 x 64 bitboard, then the list search past it;
+    list: every exact search as the list search (race_search_b3: visit marks in the labels,
+    levels staged in LDS; at n = 160 the stage holds fewer entries, so larger levels are
+    read from the HBM list)."""
     from flipcomplexityempirical_amd.chain import metropolis_table, population_bounds
     from flipcomplexityempirical_amd.graph import block_seed, grid_graph
     monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
     if variant == "list":
         monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
-    n, k = 200, 8
+    k = 8
     g = grid_graph(n, n)
     init = block_seed(n, n, 2, 4)
     bounds = population_bounds(g.total_pop, k, 0.05)
