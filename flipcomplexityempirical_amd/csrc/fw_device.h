@@ -542,6 +542,16 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
   return verdict;
 }
 
+// Where grid_race_bb2's two-class race stopped when its frontier reached the window edge:
+// per lane (grid row vr - 32 + lane, columns vc - 32 ...) the cells each class has visited
+// and its current frontier, and the direction that represents each class.  The list search
+// continues the race from here instead of from the sources (race_search_b3).
+struct BBSeed {
+  uint32_t va0, va1, vb0, vb1, fa0, fa1, fb0, fb1;
+  int ra, rb;  // representative directions (0 up, 1 left, 2 right, 3 down)
+  bool ok;
+};
+
 // grid_race_bb on a 64-row x 64-column window: lane i = grid row vr - 32 + i, bit b of
 // dword w = column vc - 32 + 32 w + b, two VGPRs per set.  The same sets, levels, merges,
 // stopping rules and counters; a window-edge frontier returns -1 as there.  Used by the
@@ -551,7 +561,8 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
 template <int LB>
 __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int lane, int vr,
                              int vc, uint32_t a, uint32_t am4, uint32_t lk, uint64_t& bfs_nodes,
-                             uint64_t& bfs_deg) {
+                             uint64_t& bfs_deg, BBSeed& sd) {
+  sd.ok = false;
   const int r = vr - 32 + lane, c0 = vc - 32;
   const bool rin = (r >= 0) & (r < H);
   const int rowb = (rin ? r : vr) * W + c0;
@@ -604,7 +615,7 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
     // test distribute over unions, and a class is closed when every direction of it is),
     // one merge test per level; the general loop's levels, stopping rules and counters
     uint32_t Fa0 = 0u, Fa1 = 0u, Fb0 = 0u, Fb1 = 0u;
-    int ra = -1;
+    int ra = -1, rb = -1;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       if (!((am4 >> d) & 1u)) continue;
@@ -616,14 +627,19 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
         Fa0 |= b0;
         Fa1 |= b1;
       } else {
+        rb = rep;
         Fb0 |= b0;
         Fb1 |= b1;
       }
     }
+    uint32_t Va0 = Fa0, Va1 = Fa1, Vb0 = Fb0, Vb1 = Fb1;  // visited, per class
     uint32_t V0 = Fa0 | Fb0, V1 = Fa1 | Fb1;
     int vd;
     for (;;) {
-      if (ballot((((Fa0 | Fb0) & E0) | ((Fa1 | Fb1) & E1)) != 0u)) return -1;
+      if (ballot((((Fa0 | Fb0) & E0) | ((Fa1 | Fb1) & E1)) != 0u)) {
+        sd = BBSeed{Va0, Va1, Vb0, Vb1, Fa0, Fa1, Fb0, Fb1, ra, rb, true};
+        return -1;
+      }
       const uint32_t Da0 = (Fa0 | (Fa0 << 1) | (Fa0 >> 1) | (Fa1 << 31) | from_prev_lane(Fa0) | from_next_lane(Fa0)) & A0;
       const uint32_t Da1 = (Fa1 | (Fa1 << 1) | (Fa1 >> 1) | (Fa0 >> 31) | from_prev_lane(Fa1) | from_next_lane(Fa1)) & A1;
       const uint32_t Db0 = (Fb0 | (Fb0 << 1) | (Fb0 >> 1) | (Fb1 << 31) | from_prev_lane(Fb0) | from_next_lane(Fb0)) & A0;
@@ -643,6 +659,10 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
       }
       V0 |= nw0;
       V1 |= nw1;
+      Va0 |= Fa0;
+      Va1 |= Fa1;
+      Vb0 |= Fb0;
+      Vb1 |= Fb1;
     }
     const uint32_t pc = (uint32_t)(__popc(V0) + __popc(V1));
     uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
@@ -755,7 +775,7 @@ struct Ctx {
   GLB uint32_t* gscr;  // LB == 3, 5: this workgroup's 4-bit visit marks in HBM (all zero
                        // between searches; such labels cannot hold the search codes)
   int32_t qcap, k;
-  int32_t scap;  // race_search_g3: next-level entries staged over the group sums (<= 128)
+  int32_t scap;  // race_search_b3: next-level entries staged over the group sums (<= 128)
   int lane;
   bool bb;  // grids: exact searches try the bitboard form first
   int my_dr, my_dc;
@@ -763,8 +783,8 @@ struct Ctx {
   uint32_t n_win = 0, n_bbs = 0, n_list = 0;  // contiguity checks by the path that decided
   uint64_t c_win = 0, c_bbs = 0, c_list = 0;  // s_memtime cycles spent in each path
   uint64_t n_bbl = 0;                          // bitboard levels run (decided or escaped)
-  uint64_t n_lvl = 0, c_atom = 0, c_clear = 0;  // list searches: levels, claim / clear cycles
-  uint64_t n_mapt = 0;                           // race_search_b3: rounds of map tests
+  uint64_t n_lvl = 0, c_clear = 0;  // race_search_b3: levels, restore cycles
+  uint64_t n_mapt = 0, n_seed = 0;  // rounds of map tests; searches seeded by the bitboard
   __device__ static __forceinline__ uint64_t now() {
     uint64_t t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1188,186 +1208,27 @@ struct Ctx {
     return verdict == 1;
   }
 
-  // The race search of 3-bit-label grids (C5's 200x200 chains, whose exact searches at
-  // steady state run ~50 levels over ~1,000 cells): race_search_gscr's levels, pushes,
-  // merges and counters with three fewer HBM round trips per level.
-  //   - The marks of the four neighbours are read together; a claim of one found empty is
-  //     one atomic OR of the class's one-hot bit (m <= 4 on a grid) into its 4-bit field,
-  //     again four in flight.  The claimer that finds the field empty pushes the node; any other finds the bits of
-  //     classes that touched it before, all of them already merged with the owner by the
-  //     end of that level, so merging with the lowest one is the merge the list search
-  //     makes.  v is skipped by id instead of marked.
-  //   - A list entry carries its class (node | class << 16), so no mark is read back.
-  //   - The next level is staged in LDS over the chain's group sums (not read while the
-  //     search runs; up to scap entries, the displaced words held in two VGPRs); every
-  //     entry also goes to the HBM visit list (write-only until the marks are cleared),
-  //     from which a level larger than the stage is read.
-  __device__ __forceinline__ void gs_or_nr(int x, uint32_t bits) const {
-    __hip_atomic_fetch_or(gscr + (x >> 3), bits << ((x & 7) << 2), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __device__ bool race_search_g3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
-                                 uint64_t& bfs_nodes, uint64_t& bfs_deg) {
-    LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
-    const uint32_t sv0 = lane < scap ? stage[lane] : 0u;
-    const uint32_t sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
-    lds_order();
-    if (lane < m) {
-      const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
-      gs_or_nr(src, 1u << lane);
-      spill[lane] = e;
-      stage[lane] = e;
-    }
-    __threadfence_block();  // the sources' marks precede every claim
-    int lb = 0, le = m;
-    uint32_t my_deg = 0;
-    uint64_t nodes = 0;
-    int verdict = -1;
-    for (;;) {
-      uint64_t rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
-      if (__popcll(rep) == 1) {
-        verdict = 1;
-        break;
-      }
-      const int cnt = le - lb;
-      const bool staged = cnt <= scap;
-      uint32_t q0 = 0u, q1 = 0u;
-      if (staged) {
-        if (lane < cnt) q0 = stage[lane];
-        if (lane + WAVE < cnt) q1 = stage[lane + WAVE];
-      }
-      lds_order();
-      uint64_t pushed_src = 0;
-      int nn = 0;
-      for (int cb = 0; cb < cnt; cb += WAVE) {
-        const int idx = cb + lane;
-        const bool act = idx < cnt;
-        uint32_t e = 0u;
-        if (staged)
-          e = cb == 0 ? q0 : q1;
-        else if (act)
-          e = spill[lb + idx];
-        const int x = (int)(e & 0xFFFFu);
-        const uint32_t o = e >> 16;
-        int xr = 0, xc = 0;
-        divmod(x, xr, xc);
-        if (act) my_deg += (uint32_t)degree(x, xr, xc);
-        nodes += (uint64_t)__popcll(ballot(act));
-        int y[4];
-        bool need[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          y[j] = act ? nbr(x, j, xr, xc) : -1;
-          need[j] = y[j] >= 0 && y[j] != v && L(y[j]) == a;
-        }
-#ifdef FW_STAMPS
-        const uint64_t t_at = now();
-#endif
-        // the marks are read first and only the cells found empty are claimed: an atomic on
-        // every a-labelled neighbour (most of them visited) measured 26% slower at C5's
-        // steady state (profiles/r03/g)
-        uint32_t got[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          got[j] = need[j] ? __hip_atomic_load(gscr + (y[j] >> 3), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (need[j] && ((got[j] >> ((y[j] & 7) << 2)) & 15u) == 0u)
-            got[j] = __hip_atomic_fetch_or(gscr + (y[j] >> 3), (1u << o) << ((y[j] & 7) << 2),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        bool pushed = false;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t nib = (got[j] >> ((y[j] & 7) << 2)) & 15u;
-          const bool push = need[j] && nib == 0u;
-          const bool req = need[j] && nib != 0u && ((nib >> o) & 1u) == 0u;
-          const uint64_t pm = ballot(push);
-          if (pm) {
-            if (push) {
-              const int slot = nn + (int)mbcnt(pm);
-              const uint32_t ent = (uint32_t)y[j] | (o << 16);
-              spill[le + slot] = ent;
-              if (slot < scap) stage[slot] = ent;
-            }
-            nn += __popcll(pm);
-          }
-          pushed |= push;
-          const uint32_t other = (uint32_t)__ffs(nib) - 1u;
-          uint64_t rm = ballot(req);
-          while (rm) {  // merges, serial over requesting lanes
-            const int Lr = __ffsll((unsigned long long)rm) - 1;
-            rm &= rm - 1;
-            const int o1 = rdl((int32_t)o, Lr), o2 = rdl((int32_t)other, Lr);
-            const uint64_t m1 = rdl64(cls, o1), m2 = rdl64(cls, o2);
-            if (m1 != m2) {
-              const uint64_t nm = m1 | m2;
-              if (lane < m && ((nm >> lane) & 1ull)) cls = nm;
-            }
-          }
-        }
-        for (int si = 0; si < m; ++si)
-          pushed_src |= ballot(pushed && o == (uint32_t)si) ? (1ull << si) : 0ull;
-#ifdef FW_STAMPS
-        c_atom += now() - t_at;
-#endif
-      }
-#ifdef FW_STAMPS
-      n_lvl += 1;
-#endif
-      lb = le;
-      le += nn;
-      if (nn > scap) __threadfence_block();  // the next level is read from the HBM list
-      lds_order();
-      rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
-      if (__popcll(rep) == 1) {
-        verdict = 1;
-        break;
-      }
-      // a class with no pushes this level is closed: disconnected
-      const bool closed = lane < m && ((rep >> lane) & 1ull) && ((cls & pushed_src) == 0ull);
-      if (ballot(closed)) {
-        verdict = 0;
-        break;
-      }
-    }
-    bfs_nodes += nodes;
-    bfs_deg += wave_sum(my_deg);
-#ifdef FW_STAMPS
-    const uint64_t t_cl = now();
-#endif
-    __threadfence_block();  // the visit list is read back
-    for (int base = 0; base < le; base += WAVE) {  // clear the marks
-      const int idx = base + lane;
-      if (idx < le) gs_clear((int)(spill[idx] & 0xFFFFu));
-    }
-    if (lane < scap) stage[lane] = sv0;
-    if (lane + WAVE < scap) stage[lane + WAVE] = sv1;
-    __threadfence_block();
-#ifdef FW_STAMPS
-    c_clear += now() - t_cl;
-#endif
-    return verdict == 1;
-  }
-
-  // The race search of 3-bit-label grids with its visit marks in the labels themselves:
-  // the same levels, pushes, merges and counters as race_search_gscr (the oracle's
-  // contiguous_after), with LDS round trips where that search pays HBM ones.  A claimed
-  // node's label a becomes its class's code c_o; codes are the unused labels k..7 first,
-  // then borrowed district labels.  A borrowed code is ambiguous (a node of that district,
+  // The race search of 3-bit-label grids (C5's 200x200 chains) with its visit marks in the
+  // labels themselves: the levels, pushes, merges and counters of race_search_gscr and of
+  // the oracle's contiguous_after, with LDS round trips where an HBM-marked search pays
+  // memory-side atomics (global atomics execute past the XCD's L2).  A claimed node's label
+  // a becomes its class's code: the unused labels k..7 first, then district labels absent
+  // from a 256-cell sample around v.  A borrowed code is ambiguous (a cell of that district,
   // or a visited one), so claims under it also set the node's byte in an HBM map (n bytes
-  // per workgroup), read only when a frontier node of another, unmerged class meets the
-  // code: the merge test.  Within a
-  // level the four neighbour directions run one after another, so a node claimed in an
-  // earlier direction reads as claimed (LDS ops of one wave execute in program order) and
-  // no node is pushed twice: on a grid, two frontier nodes reach the same node in one
-  // direction only if they are the same node.  The ambiguous merge tests of a chunk are
-  // resolved together after it (merges are unions: their order within a level does not
-  // change the classes at its end).  Labels and map bits are restored from the HBM visit
-  // list at the end; levels are staged in LDS over the group sums as in race_search_g3.
+  // per workgroup, plain byte stores), read (L2-served sc1 loads, after the stores drained)
+  // only when a frontier node of another, unmerged class meets the code: the merge test.
+  // Within a level the four neighbour directions run one after another, so a node claimed
+  // in an earlier direction reads as claimed (LDS ops of one wave execute in program order)
+  // and no node is pushed twice: on a grid two frontier nodes reach the same node in one
+  // direction only if they are the same node.  A list entry carries its class (node |
+  // class << 16).  The next level is staged in LDS over the chain's group sums (not read
+  // while the search runs; up to scap entries, the displaced words held in two VGPRs) and
+  // every entry goes to the HBM visit list, from which a larger level is read and the
+  // labels and map bytes are restored at the end.  With a seed (grid_race_bb2's two-class
+  // race left its 64 x 64 window), the race continues from the bitboard's visited cells and
+  // frontier instead of from the sources.
   __device__ bool race_search_b3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
-                                 uint64_t& bfs_nodes, uint64_t& bfs_deg) {
+                                 const BBSeed& sd, uint64_t& bfs_nodes, uint64_t& bfs_deg) {
     LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
     // the map: one byte per node, set and cleared by plain byte stores (global atomics
     // execute past the XCD's L2 and drop the line), read by L2-served sc1 loads after the
@@ -1420,7 +1281,64 @@ struct Ctx {
     const uint32_t sv0 = lane < scap ? stage[lane] : 0u;
     const uint32_t sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
     lds_order();
-    if (lane < m) {
+    int lb = 0, le = m;
+    uint32_t my_deg = 0;
+    uint64_t nodes = 0;
+    if (sd.ok) {
+      // continue grid_race_bb2's race where it left its window: its visited cells take
+      // their class's code and form the head of the visit list (the processed cells, counted
+      // as the bitboard counts them), its frontier the current level
+#ifdef FW_STAMPS
+      n_seed += 1;
+#endif
+      int vr, vc;
+      divmod(v, vr, vc);
+      const int r = vr - 32 + lane, c0 = vc - 32;
+      const uint32_t pa0 = sd.va0 & ~sd.fa0, pa1 = sd.va1 & ~sd.fa1;
+      const uint32_t pb0 = sd.vb0 & ~sd.fb0, pb1 = sd.vb1 & ~sd.fb1;
+      const uint32_t c1 = (uint32_t)(__popc(pa0) + __popc(pa1) + __popc(pb0) + __popc(pb1));
+      const uint32_t c2 = (uint32_t)(__popc(sd.fa0) + __popc(sd.fa1) + __popc(sd.fb0) + __popc(sd.fb1));
+      const uint32_t i1 = scan_incl(c1), i2 = scan_incl(c2);
+      const int n1 = (int)rdl(i1, 63), n2 = (int)rdl(i2, 63);
+      const uint32_t ca = (codes >> (3 * sd.ra)) & 7u, cb = (codes >> (3 * sd.rb)) & 7u;
+      const bool ma = (ambig >> sd.ra) & 1u, mb = (ambig >> sd.rb) & 1u;
+      // one class's cells of one dword of this lane's row, from list index idx on
+      auto emit = [&](uint32_t bits, int col, uint32_t o, uint32_t code, bool amb, int& idx,
+                      bool staged) {
+        while (bits) {
+          const int t = __ffs(bits) - 1;
+          bits &= bits - 1;
+          const int x = r * g.gw + col + t;
+          const uint32_t e = (uint32_t)x | (o << 16);
+          spill[idx] = e;
+          if (staged && idx - n1 < scap) stage[idx - n1] = e;
+          P::axor(lab, x, a ^ code);
+          if (amb) bmap[x] = 1u;
+          ++idx;
+        }
+      };
+      int idx = (int)(i1 - c1);
+      emit(pa0, c0, (uint32_t)sd.ra, ca, ma, idx, false);
+      emit(pa1, c0 + 32, (uint32_t)sd.ra, ca, ma, idx, false);
+      emit(pb0, c0, (uint32_t)sd.rb, cb, mb, idx, false);
+      emit(pb1, c0 + 32, (uint32_t)sd.rb, cb, mb, idx, false);
+      idx = n1 + (int)(i2 - c2);
+      emit(sd.fa0, c0, (uint32_t)sd.ra, ca, ma, idx, true);
+      emit(sd.fa1, c0 + 32, (uint32_t)sd.ra, ca, ma, idx, true);
+      emit(sd.fb0, c0, (uint32_t)sd.rb, cb, mb, idx, true);
+      emit(sd.fb1, c0 + 32, (uint32_t)sd.rb, cb, mb, idx, true);
+      // the bitboard's counters over the processed cells (grid_race_bb2)
+      const uint32_t q0 = pa0 | pb0, q1 = pa1 | pb1;
+      uint32_t dg = c1 * (uint32_t)((r > 0) + (r < g.gh - 1) + 2);
+      auto qbit = [&](int pos) { return pos < 32 ? (q0 >> pos) & 1u : (q1 >> (pos - 32)) & 1u; };
+      if (c0 <= 0) dg -= qbit(-c0);
+      if (g.gw - c0 <= 64) dg -= qbit(g.gw - c0 - 1);
+      my_deg += dg;
+      nodes += (uint64_t)n1;
+      lb = n1;
+      le = n1 + n2;
+      if (n2 > scap) __threadfence_block();  // the level is read from the HBM list
+    } else if (lane < m) {
       const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
       P::axor(lab, src, a ^ ((codes >> (3 * lane)) & 7u));
       if ((ambig >> lane) & 1u) bmap[src] = 1u;
@@ -1428,9 +1346,6 @@ struct Ctx {
       stage[lane] = e;
     }
     lds_order();
-    int lb = 0, le = m;
-    uint32_t my_deg = 0;
-    uint64_t nodes = 0;
     int verdict = -1;
     for (;;) {
       if (n_classes() == 1) {
@@ -1703,6 +1618,8 @@ struct Ctx {
     if (m == 1) return true;
     CTX_T0
     uint64_t cls = lane < m ? (1ull << lane) : 0ull;
+    BBSeed sd;
+    sd.ok = false;
     // source index (rank in am) of the source held by lane ln
     auto sx = [&](int ln) { return __popcll(am & ((1ull << ln) - 1ull)); };
     auto merge = [&](int s1, int s2) {
@@ -1715,23 +1632,21 @@ struct Ctx {
       // nbadj has the padded [n][16] layout whenever the padded table exists
       const size_t e0 = (E16 || g.ell) ? (size_t)v * 16 : (size_t)g.rowptr[v];
       const uint64_t adjl = ((am >> lane) & 1ull) ? (g.nbadj[e0 + lane - 1] << 1) & am : 0ull;
-      uint64_t comp = am & (~am + 1ull);  // the lowest source
-      for (;;) {
-        const uint64_t nxt = comp | wave_or64(((comp >> lane) & 1ull) ? adjl : 0ull);
-        if (nxt == comp) break;
-        comp = nxt;
-      }
-      if (comp == am) return true;
-      uint64_t todo = am;
-      while (todo) {
-        const int Ls = __ffsll((unsigned long long)todo) - 1;
-        todo &= todo - 1;
-        uint64_t nb = rdl64(adjl, Ls) & ~((2ull << Ls) - 1ull);  // each pair once
-        while (nb) {
-          const int Lt = __ffsll((unsigned long long)nb) - 1;
-          nb &= nb - 1;
-          merge(sx(Ls), sx(Lt));
+      // components of the sources' adjacency, one ballot per closure step: the relation
+      // is symmetric, so a source joins when its own row meets the component
+      uint64_t rest = am;
+      for (bool first = true; rest; first = false) {
+        uint64_t comp = rest & (~rest + 1ull);  // the lowest source left
+        for (;;) {
+          const uint64_t nxt = comp | ballot((adjl & comp) != 0ull);
+          if (nxt == comp) break;
+          comp = nxt;
         }
+        if (first && comp == am) return true;
+        rest &= ~comp;
+        const int L0 = __ffsll((unsigned long long)comp) - 1;
+        for (uint64_t t = comp & (comp - 1ull); t; t &= t - 1ull)
+          merge(sx(L0), sx(__ffsll((unsigned long long)t) - 1));
       }
     }
     if constexpr (GRID) {
@@ -1759,13 +1674,22 @@ struct Ctx {
       if (bb) {  // bitboard search first; the list search past its window
         int vr, vc;
         divmod(v, vr, vc);
-        // 3-bit labels (large grids, C5): the 64-column window
+        // 3-bit labels (large grids, C5): the 64-column window, whose two-class race hands
+        // its state to the list search when it leaves the window
         const uint32_t am4 = (uint32_t)(am >> 1) & 15u;
         const uint32_t lk = (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3));
-        const int wv = LB == 3 ? grid_race_bb2<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk,
-                                                   bfs_nodes, bfs_deg)
-                               : grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk,
-                                                  bfs_nodes, bfs_deg);
+        int wv;
+        if constexpr (LB == 3) {
+          wv = grid_race_bb2<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk, bfs_nodes,
+                                 bfs_deg, sd);
+          if (sd.ok) {  // the classes' source indices (CSR order of v's neighbours)
+            sd.ra = sx(sd.ra + 1);
+            sd.rb = sx(sd.rb + 1);
+          }
+        } else {
+          wv = grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk, bfs_nodes,
+                                bfs_deg);
+        }
 #ifdef FW_STAMPS
         n_bbs += 1;
 #endif
@@ -1795,16 +1719,9 @@ struct Ctx {
       if (lane == i) src = val;
     }
     bool verdict;
-#ifndef FW_G3_OFF
     if constexpr (LB == 3 && GRID)
-#ifdef FW_G3
-      verdict = race_search_g3(v, a, m, src, cls, scap, bfs_nodes, bfs_deg);
-#else
-      verdict = race_search_b3(v, a, m, src, cls, scap, bfs_nodes, bfs_deg);
-#endif
-    else
-#endif
-    if constexpr (LB == 3 || LB == 5)
+      verdict = race_search_b3(v, a, m, src, cls, scap, sd, bfs_nodes, bfs_deg);
+    else if constexpr (LB == 3 || LB == 5)
       verdict = race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else
       verdict = race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);

@@ -478,7 +478,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   CSTAMP_COUNT(12, C.c_bbs);
   CSTAMP_COUNT(13, C.c_list);
   CSTAMP_COUNT(6, C.n_lvl);
-  CSTAMP_COUNT(7, C.c_atom);
+  CSTAMP_COUNT(7, C.n_seed);
   CSTAMP_COUNT(14, C.c_clear);
   CSTAMP_COUNT(15, C.n_mapt);
 #endif
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(64) void fw_eval_kernel(FwEvalParams p) {
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.qcap = p.qcap;
-  C.scap = 0;  // 4- and 8-bit labels only: race_search_g3 is not instantiated
+  C.scap = 0;  // 4- and 8-bit labels only: race_search_b3 is not instantiated
   C.k = p.k;
   C.bb = true;
   C.init_roles();

@@ -66,9 +66,9 @@ if cb[:6].sum():
           f"{cb[9] / att:.3f}, list search {cb[10] / att:.3f}")
     if cb[6]:
         print(f"list search: {cb[6] / max(cb[10], 1):.1f} levels per run, "
-              f"claim+merge {cb[7] / cb[6]:.0f} clk per level (race_search_g3), "
-              f"map-test rounds {cb[15] / cb[6]:.2f} per level (race_search_b3), "
-              f"clearing {cb[14] / max(cb[10], 1):.0f} clk per run")
+              f"{cb[7] / max(cb[10], 1):.2f} of the runs seeded by the bitboard, "
+              f"map-test rounds {cb[15] / cb[6]:.2f} per level, "
+              f"restore {cb[14] / max(cb[10], 1):.0f} clk per run")
     if cb[11] + cb[12] + cb[13]:
         print(f"contiguity cycles by path (per attempt / per run): 7x7 window "
               f"{cb[11] / att:.0f} / {cb[11] / max(cb[8], 1):.0f}, bitboard {cb[12] / att:.0f} / "
