@@ -75,6 +75,26 @@ __device__ __forceinline__ uint32_t scan_incl(uint32_t x) {
 }
 // wave-wide sum, returned uniform
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return rdl(scan_incl(x), 63); }
+// wave-wide OR / max of 32-bit values with the DPP pattern of scan_incl (no LDS round
+// trips; wave_or64's ds_bpermute steps each wait on the LDS pipe), returned uniform
+__device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return rdl(x, 63);
+}
+__device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+  return rdl(x, 63);
+}
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) x |= __shfl_xor(x, d, WAVE);
@@ -1140,10 +1160,7 @@ struct Ctx {
         bfs_nodes += (uint64_t)__popcll(ballot(act));
         int jmax = 4;
         if constexpr (!GRID) {
-          uint32_t dm = (uint32_t)dmax;
-#pragma unroll
-          for (int dd = 32; dd >= 1; dd >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, dd, WAVE));
-          jmax = (int)rfl(dm);
+          jmax = (int)wave_max32((uint32_t)dmax);
         }
         for (int j = 0; j < (E16 ? 16 : 64); ++j) {  // r16[j]: uniform j
           if (j >= jmax) break;  // uniform
@@ -1249,7 +1266,7 @@ struct Ctx {
         const int rr = vr + 4 * (cell >> 4) - 30, cc = vc + 4 * (cell & 15) - 30;
         if (rr >= 0 && rr < g.gh && cc >= 0 && cc < g.gw) seen |= 1u << L(rr * g.gw + cc);
       }
-      seen = (uint32_t)wave_or64(seen);
+      seen = wave_or32(seen);
       int o = 0;
       for (uint32_t c = (uint32_t)k; c < 8u && o < m; ++c, ++o) codes |= c << (3 * o);
       for (int pass = 0; pass < 2; ++pass)  // absent labels first, then present ones
@@ -1347,7 +1364,101 @@ struct Ctx {
     }
     lds_order();
     int verdict = -1;
-    for (;;) {
+    if (sd.ok) {
+      // the seeded race has two classes: one code test per neighbour, a merge ends it
+      const uint32_t oa = (uint32_t)sd.ra;
+      const uint32_t ca = (codes >> (3 * sd.ra)) & 7u, cb = (codes >> (3 * sd.rb)) & 7u;
+      const bool ma = (ambig >> sd.ra) & 1u, mb = (ambig >> sd.rb) & 1u;
+      for (;;) {
+        const int cnt = le - lb;
+        const bool staged = cnt <= scap;
+        uint32_t q0 = 0u, q1 = 0u;
+        if (staged) {
+          if (lane < cnt) q0 = stage[lane];
+          if (lane + WAVE < cnt) q1 = stage[lane + WAVE];
+        }
+        lds_order();
+        bool merged = false, pa = false, pb = false;
+        int nn = 0;
+        for (int cb0 = 0; cb0 < cnt; cb0 += WAVE) {
+          const int idx = cb0 + lane;
+          const bool act = idx < cnt;
+          uint32_t e = 0u;
+          if (staged)
+            e = cb0 == 0 ? q0 : q1;
+          else if (act)
+            e = spill[lb + idx];
+          const int x = (int)(e & 0xFFFFu);
+          const uint32_t o = e >> 16;
+          const bool isa = o == oa;
+          const uint32_t co = isa ? ca : cb, cother = isa ? cb : ca;
+          const bool amb_o = isa ? ma : mb, amb_other = isa ? mb : ma;
+          int xr = 0, xc = 0;
+          divmod(x, xr, xc);
+          if (act) my_deg += (uint32_t)degree(x, xr, xc);
+          nodes += (uint64_t)__popcll(ballot(act));
+          bool pushed = false, met = false;
+          uint32_t chk = 0;
+          int ys[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int y = act ? nbr(x, j, xr, xc) : -1;
+            ys[j] = y;
+            const bool ok = y >= 0 && y != v;
+            const uint32_t ly = L(ok ? y : x);
+            const bool push = ok && ly == a;
+            if (push) P::axor(lab, y, a ^ co);
+            const uint64_t pm = ballot(push);
+            if (pm) {
+              if (push) {
+                if (amb_o) bmap[y] = 1u;
+                const int slot = nn + (int)mbcnt(pm);
+                const uint32_t ent = (uint32_t)y | (o << 16);
+                spill[le + slot] = ent;
+                if (slot < scap) stage[slot] = ent;
+              }
+              nn += __popcll(pm);
+            }
+            pushed |= push;
+            const bool oth = ok && ly == cother;  // the other class, or (ambiguous) a district
+            met |= oth && !amb_other;
+            if (oth && amb_other) chk |= 1u << j;
+          }
+          merged |= ballot(met) != 0ull;
+          if (!merged && ballot(chk != 0u)) {  // map tests after this chunk's stores drained
+#ifdef FW_STAMPS
+            n_mapt += 1;
+#endif
+            __threadfence_block();
+            bool hit = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if ((chk >> j) & 1u)
+                hit |= ((__hip_atomic_load(bm + (ys[j] >> 2), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) >> ((ys[j] & 3) << 3)) & 0xFFu) != 0u;
+            merged |= ballot(hit) != 0ull;
+          }
+          pa |= ballot(pushed && isa) != 0ull;
+          pb |= ballot(pushed && !isa) != 0ull;
+        }
+#ifdef FW_STAMPS
+        n_lvl += 1;
+#endif
+        lb = le;
+        le += nn;
+        if (nn > scap) __threadfence_block();  // the next level is read from the HBM list
+        lds_order();
+        if (merged) {  // one class: connected
+          verdict = 1;
+          break;
+        }
+        if (!pa || !pb) {  // a class pushed nothing: closed, disconnected
+          verdict = 0;
+          break;
+        }
+      }
+    }
+    for (; verdict < 0;) {
       if (n_classes() == 1) {
         verdict = 1;
         break;
@@ -1533,10 +1644,7 @@ struct Ctx {
         bfs_nodes += (uint64_t)__popcll(ballot(act));
         int jmax = 4;
         if constexpr (!GRID) {
-          uint32_t dm = (uint32_t)dmax;
-#pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) dm = max(dm, (uint32_t)__shfl_xor(dm, d, WAVE));
-          jmax = (int)rfl(dm);
+          jmax = (int)wave_max32((uint32_t)dmax);
         }
         for (int j = 0; j < (E16 ? 16 : 64); ++j) {  // r16[j]: uniform j (v_movrels)
           if (j >= jmax) break;  // uniform

@@ -314,7 +314,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
               mask |= (ll != a && ll != NOLAB) ? (1ull << ll) : 0ull;
             }
           } else {
-            mask = rfl64(wave_or64((isnb && h.lx != a) ? (1ull << h.lx) : 0ull));
+            // the foreign labels among v's neighbours (DPP OR when they fit 32 bits)
+            if (k <= 32)
+              mask = wave_or32((isnb && h.lx != a) ? (1u << h.lx) : 0u);
+            else
+              mask = rfl64(wave_or64((isnb && h.lx != a) ? (1ull << h.lx) : 0ull));
           }
           d = (uint32_t)nth_bit(mask, j);
         }
