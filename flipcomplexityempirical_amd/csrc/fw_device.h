@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fw_internal.h"
 #include "fw_math.h"
 
@@ -358,14 +360,18 @@ __device__ __forceinline__ void role_off(int l, int& dr, int& dc) {
 }
 
 // What one lane learns about its node x of v's neighbourhood.
-struct Hood {
+// MT: the label-set mask, 32 bits wherever labels are below 32 (every width but 8 bits)
+template <typename MT>
+struct HoodT {
   int x;          // node id, -1 if absent
   uint32_t lx;    // label of x (NOLAB if absent)
-  uint64_t bits;  // OR of 1<<label over x's neighbours other than v
+  MT bits;        // OR of 1<<label over x's neighbours other than v
   uint32_t cnt;   // number of x's neighbours other than v with label != lx
   bool has_v;     // v is a neighbour of x
   int deg;        // degree of x
 };
+__device__ __forceinline__ uint32_t popcnt(uint32_t x) { return (uint32_t)__popc(x); }
+__device__ __forceinline__ uint32_t popcnt(uint64_t x) { return (uint32_t)__popcll(x); }
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
@@ -787,6 +793,8 @@ __device__ __forceinline__ int gsum_slot(int g) {
 template <int LB, bool GRID, bool E16 = false>
 struct Ctx {
   using P = PK<LB>;
+  using MaskT = typename std::conditional<LB == 8, uint64_t, uint32_t>::type;
+  using Hood = HoodT<MaskT>;
   FwGraphDev g;
   LDS uint8_t* lab;
   LDS uint16_t* gsum;  // u16 group sums (<= 64 nodes x weight <= 63), gsum_slot layout
@@ -878,7 +886,7 @@ struct Ctx {
     int xr = 0, xc = 0;
     if constexpr (GRID) divmod(x, xr, xc);
     const uint32_t lx = L(x);
-    uint64_t bits = 0;
+    MaskT bits = 0;
     cd = 0;
     if constexpr (E16) {
       int r[16];
@@ -888,10 +896,10 @@ struct Ctx {
         if (j >= g.maxdeg) break;  // uniform
         const int y = r[j];
         const uint32_t ly = L(y >= 0 ? y : x);
-        bits |= y >= 0 ? 1ull << ly : 0ull;
+        bits |= y >= 0 ? MaskT(1) << ly : MaskT(0);
         cd += (y >= 0 && ly != lx) ? 1u : 0u;
       }
-      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : (uint32_t)__popcll(bits & ~(1ull << lx));
+      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : popcnt(bits & ~(MaskT(1) << lx));
       return;
     }
     if constexpr (GRID) {
@@ -899,11 +907,12 @@ struct Ctx {
       const bool hu = xr > 0, hl = xc > 0, hr = xc < g.gw - 1, hd = xr < g.gh - 1;
       const uint32_t lu = L(hu ? x - g.gw : x), ll = L(hl ? x - 1 : x);
       const uint32_t lr = L(hr ? x + 1 : x), ld = L(hd ? x + g.gw : x);
-      bits = (hu ? 1ull << lu : 0ull) | (hl ? 1ull << ll : 0ull) | (hr ? 1ull << lr : 0ull) |
-             (hd ? 1ull << ld : 0ull);
+      const MaskT one = 1;
+      bits = (hu ? one << lu : 0) | (hl ? one << ll : 0) | (hr ? one << lr : 0) |
+             (hd ? one << ld : 0);
       cd = (uint32_t)(hu & (lu != lx)) + (uint32_t)(hl & (ll != lx)) + (uint32_t)(hr & (lr != lx)) +
            (uint32_t)(hd & (ld != lx));
-      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : (uint32_t)__popcll(bits & ~(1ull << lx));
+      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : popcnt(bits & ~(one << lx));
       return;
     }
     const int dx = g.rowptr[x + 1] - g.rowptr[x];
@@ -911,10 +920,10 @@ struct Ctx {
       const int y = nbr(x, j, xr, xc);
       if (y < 0) continue;
       const uint32_t ly = L(y);
-      bits |= 1ull << ly;
+      bits |= MaskT(1) << ly;
       cd += ly != lx;
     }
-    w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : (uint32_t)__popcll(bits & ~(1ull << lx));
+    w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : popcnt(bits & ~(MaskT(1) << lx));
   }
 
   // Weights of v's neighbourhood before and after v: a -> d (lane roles above).
@@ -930,8 +939,8 @@ struct Ctx {
         wo = (uint32_t)(h.deg - m);
         wn = (uint32_t)(h.deg - nb);
       } else {
-        wo = (uint32_t)__popcll(h.bits & ~(1ull << a));
-        wn = (uint32_t)__popcll(h.bits & ~(1ull << d));
+        wo = popcnt(h.bits & ~(MaskT(1) << a));
+        wn = popcnt(h.bits & ~(MaskT(1) << d));
       }
       return;
     }
@@ -939,9 +948,9 @@ struct Ctx {
       wo = h.cnt + (h.has_v && a != h.lx);
       wn = h.cnt + (h.has_v && d != h.lx);
     } else {
-      const uint64_t keep = ~(1ull << h.lx);
-      wo = (uint32_t)__popcll((h.bits | (h.has_v ? 1ull << a : 0ull)) & keep);
-      wn = (uint32_t)__popcll((h.bits | (h.has_v ? 1ull << d : 0ull)) & keep);
+      const MaskT keep = ~(MaskT(1) << h.lx);
+      wo = popcnt((h.bits | (h.has_v ? MaskT(1) << a : MaskT(0))) & keep);
+      wn = popcnt((h.bits | (h.has_v ? MaskT(1) << d : MaskT(0))) & keep);
     }
   }
 
@@ -978,8 +987,9 @@ struct Ctx {
         const bool vu = lane == 4, vl = lane == 3, vrr = lane == 2, vd = lane == 1;
         h.has_v = lane > 0;
         const bool uu = hu & !vu, ul = hl & !vl, ur = hr & !vrr, ud = hd & !vd;
-        h.bits = (uu ? 1ull << lu : 0ull) | (ul ? 1ull << ll : 0ull) | (ur ? 1ull << lr : 0ull) |
-                 (ud ? 1ull << ld : 0ull);
+        const MaskT one = 1;
+        h.bits = (uu ? one << lu : 0) | (ul ? one << ll : 0) | (ur ? one << lr : 0) |
+                 (ud ? one << ld : 0);
         h.cnt = (uint32_t)(uu & (lu != lxx)) + (uint32_t)(ul & (ll != lxx)) +
                 (uint32_t)(ur & (lr != lxx)) + (uint32_t)(ud & (ld != lxx));
       }
@@ -1001,7 +1011,7 @@ struct Ctx {
         const uint32_t ly = L(ok ? y : h.x);
         deg += y >= 0 ? 1 : 0;
         h.has_v = h.has_v || y == v;
-        h.bits |= ok ? 1ull << ly : 0ull;
+        h.bits |= ok ? MaskT(1) << ly : MaskT(0);
         h.cnt += (ok && ly != h.lx) ? 1u : 0u;
       }
       h.deg = deg;
@@ -1021,7 +1031,7 @@ struct Ctx {
           continue;
         }
         const uint32_t ly = L(y);
-        h.bits |= 1ull << ly;
+        h.bits |= MaskT(1) << ly;
         h.cnt += ly != h.lx;
       }
     }

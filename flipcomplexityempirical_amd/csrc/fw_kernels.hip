@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       uint32_t a = 0, d = 0;
       int64_t pv = 1;
       U4 x;
-      Hood h;
+      typename Ctx<LB, GRID, E16>::Hood h;
       bool valid = false;
       for (;;) {
         CSTAMP(-1);
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(64) void fw_eval_kernel(FwEvalParams p) {
     const int v = p.v[i];
     const uint32_t b = (uint32_t)p.target[i];
     int dv = 0;
-    const Hood h = C.gather(v, dv);
+    const auto h = C.gather(v, dv);
     const uint32_t a = rfl(rdl(h.lx, 0));
     const bool isnb = GRID ? (lane >= 1 && lane <= 4 && h.x >= 0) : (lane >= 1 && lane <= dv);
     const uint64_t am = ballot(isnb && h.lx == a);
