@@ -3,7 +3,7 @@
 # the steady-state protocol (10/100) on every workload, and the C5 8-GPU job emulated shard
 # by shard at the steady-state protocol.  Output under gpurun_out/r03v/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r03v
+O=${R03V_OUT:-gpurun_out/r03v}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?
