@@ -880,28 +880,38 @@ struct Ctx {
     }
   }
 
+  // E16: proposal weight and cut degree of x from its padded row, walking md entries
+  // (wave-uniform, >= x's degree: the rest of a row is -1 padding)
+  template <int MODE>
+  __device__ __forceinline__ void weight_row(int x, int md, uint32_t& w, uint32_t& cd) const {
+    int r[16];
+    row16(x, r);
+    const uint32_t lx = L(x);
+    MaskT bits = 0;
+    cd = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j >= md) break;  // uniform
+      const int y = r[j];
+      const uint32_t ly = L(y >= 0 ? y : x);
+      bits |= y >= 0 ? MaskT(1) << ly : MaskT(0);
+      cd += (y >= 0 && ly != lx) ? 1u : 0u;
+    }
+    w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : popcnt(bits & ~(MaskT(1) << lx));
+  }
+
   // Proposal weight and cut degree of x under the current labels.
   template <int MODE>
   __device__ __forceinline__ void weight_now(int x, uint32_t& w, uint32_t& cd) const {
+    if constexpr (E16) {
+      weight_row<MODE>(x, g.maxdeg, w, cd);
+      return;
+    }
     int xr = 0, xc = 0;
     if constexpr (GRID) divmod(x, xr, xc);
     const uint32_t lx = L(x);
     MaskT bits = 0;
     cd = 0;
-    if constexpr (E16) {
-      int r[16];
-      row16(x, r);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (j >= g.maxdeg) break;  // uniform
-        const int y = r[j];
-        const uint32_t ly = L(y >= 0 ? y : x);
-        bits |= y >= 0 ? MaskT(1) << ly : MaskT(0);
-        cd += (y >= 0 && ly != lx) ? 1u : 0u;
-      }
-      w = (MODE == FW_PROPOSE_CUTEDGE) ? cd : popcnt(bits & ~(MaskT(1) << lx));
-      return;
-    }
     if constexpr (GRID) {
       // branch-free: the four reads issued together at clamped positions, then masked
       const bool hu = xr > 0, hl = xc > 0, hr = xc < g.gw - 1, hd = xr < g.gh - 1;
@@ -994,7 +1004,13 @@ struct Ctx {
                 (uint32_t)(ur & (lr != lxx)) + (uint32_t)(ud & (ld != lxx));
       }
     } else if constexpr (E16) {
-      // lanes 1..16 read v's padded row: its neighbours (a prefix) and so its degree
+      // lanes 1..16 read v's padded row: its neighbours (a prefix) and so its degree; the
+      // rows below are walked up to the largest degree among v and its neighbours
+#ifdef FW_VAR_NODB
+      const int md = g.maxdeg;
+#else
+      const int md = rfl(g.dbound[v]);
+#endif
       const int xn = (lane >= 1 && lane <= 16) ? g.ell[(size_t)v * 16 + lane - 1] : -1;
       dv = __popcll(ballot(xn >= 0));
       if (lane > dv) return h;
@@ -1005,7 +1021,7 @@ struct Ctx {
       int deg = 0;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        if (j >= g.maxdeg) break;  // uniform
+        if (j >= md) break;  // uniform
         const int y = r[j];
         const bool ok = y >= 0 && y != v;
         const uint32_t ly = L(ok ? y : h.x);
@@ -1085,7 +1101,17 @@ struct Ctx {
     }
     const int x = gi * 64 + lane;
     uint32_t wx = 0, cd;
-    if (x < g.n) weight_now<MODE>(x, wx, cd);
+    if constexpr (E16) {
+      // the group's rows are walked up to its largest degree (C4: 9.7 on average, not 14)
+#ifdef FW_VAR_NODB
+      const int md = g.maxdeg;
+#else
+      const int md = rfl(g.dbound[g.n + gi]);
+#endif
+      if (x < g.n) weight_row<MODE>(x, md, wx, cd);
+    } else {
+      if (x < g.n) weight_now<MODE>(x, wx, cd);
+    }
     const uint32_t incl2 = scan_incl(wx);
     const uint64_t m2 = ballot(incl2 > r1);
     if (m2 == 0) {

@@ -21,6 +21,8 @@ struct FwGraphDev {
   const int32_t* eid;     // [nnz] canonical edge id of each CSR entry
   const uint64_t* nbadj;  // [nnz] entry (v, i): bit j set iff neighbours i and j of v are adjacent
   const int32_t* ell;     // [n][16] neighbours padded with -1 (general graphs, max degree <= 16)
+  const int32_t* dbound;  // with ell: [n] max degree over x and its neighbours, then
+                          // [ceil(n/64)] max degree in each 64-node group (row loop bounds)
   const int64_t* pop;     // [n] or nullptr (unit populations)
   const double* invb;     // [n+1] 1.0 / max(b, 1), correctly rounded (no fp64 divide per step)
   int32_t n, nedges, maxdeg;
