@@ -240,6 +240,8 @@ def main():
     ap.add_argument("--ladder", default="interleaved", choices=["interleaved", "contiguous"],
                     help="C5: base groups spread over the shards in snake order of the ladder octaves "
                          "(default, workloads.ladder_base_index) or adjacent (round 1)")
+    ap.add_argument("--order", default=None, choices=["random", "hilbert"],
+                    help="C4: node numbering of the Delaunay graph (workloads.C4_ORDER by default)")
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--base", type=float, default=None)
@@ -263,10 +265,17 @@ def main():
                          "timing and profiling without the burn-in launches")
     ap.add_argument("--save-checkpoint", default=None, metavar="NPZ",
                     help="write the chains (Chains.save_checkpoint) after the timed launches")
+    ap.add_argument("--save-hist", default=None, metavar="NPZ",
+                    help="rank 0 writes the merged histograms (hist_cut, hist_b) and the "
+                         "gathered per-chain final cut / |B| to this file")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
                     help="per-launch HBM bytes from a rocprofv3 PMC pass of the default C3 "
                          "command (scripts/profile.sh -> scripts/pmc_summary.py)")
     args = ap.parse_args()
+    if args.maps and args.resume:
+        # fw_chains_write refuses plan writes while maps are on, and maps cannot be enabled
+        # after a restore (the handle has run): checkpoints do not carry the per-node maps
+        ap.error("--maps cannot be combined with --resume (checkpoints carry no spatial maps)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -287,7 +296,7 @@ def main():
     from flipcomplexityempirical_amd.chain import Chains, DeviceGraph, population_bounds
     from flipcomplexityempirical_amd.distributed import merge_histograms, shard_range
 
-    w = workload(args.config, args.grid, args.k)
+    w = workload(args.config, args.grid, args.k, args.order)
     w.interleave = args.ladder == "interleaved"
     g, init, k = w.graph, w.init, w.k
     proposal = args.proposal or w.proposal
@@ -373,6 +382,14 @@ def main():
 
     if args.save_checkpoint:
         ch.save_checkpoint(args.save_checkpoint)
+    if args.save_hist:
+        fin = np.stack([st1_arr["cut"], st1_arr["bnodes"]]).astype(np.int64)
+        if dist is not None:
+            parts = [None] * world
+            dist.all_gather_object(parts, fin)
+            fin = np.concatenate(parts, axis=1)
+        if rank == 0:
+            np.savez(args.save_hist, hist_cut=hist_cut, hist_b=hist_b, final=fin)
     kernel_ms = float(np.mean(kms))
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9

@@ -316,7 +316,8 @@ class Chains:
         ck = {"labels": self.labels(), "stats": self.stats(), "hist_cut": self.hist_cut(),
               "hist_b": self.hist_b(), "seed": np.uint64(self.seed),
               "chain_id0": np.int64(self.chain_id0), "thr": self.thr,
-              "mode": np.int32(self.mode), "accept_rule": np.int32(self.accept_rule)}
+              "mode": np.int32(self.mode), "accept_rule": np.int32(self.accept_rule),
+              "pop_lo": np.int64(self.pop_lo), "pop_hi": np.int64(self.pop_hi)}
         if self.node_flags is not None:
             ck["node_flags"] = self.node_flags
         if self._sched is not None:
@@ -336,6 +337,12 @@ class Chains:
         if "mode" in ck and int(ck["mode"]) != self.mode:
             raise ValueError(f"checkpoint of proposal mode {int(ck['mode'])}, handle has "
                              f"{self.mode}")
+        if "pop_lo" in ck and (int(ck["pop_lo"]), int(ck["pop_hi"])) != (self.pop_lo, self.pop_hi):
+            raise ValueError(f"checkpoint of population bounds [{int(ck['pop_lo'])}, "
+                             f"{int(ck['pop_hi'])}], handle has [{self.pop_lo}, {self.pop_hi}]")
+        if self.waits_on and "waits" not in ck:
+            raise ValueError("sampled waits are enabled but the checkpoint carries none: the "
+                             "resumed sums would miss every earlier yield")
         L = _lib.load()
         if "waits" in ck and not self.waits_on:
             self.enable_sampled_waits()
@@ -357,7 +364,16 @@ class Chains:
         # the accept rule and the bound schedule the checkpointed chains ran under (after the
         # plans: the boundary rule's flagged-node counts are taken from them)
         if "accept_rule" in ck:
-            self.set_accept(int(ck["accept_rule"]), ck.get("node_flags"))
+            rule, fl = int(ck["accept_rule"]), ck.get("node_flags")
+            same = rule == self.accept_rule and (
+                (fl is None and self.node_flags is None) or
+                (fl is not None and self.node_flags is not None and
+                 np.array_equal(np.asarray(fl, np.uint8), self.node_flags)))
+            # the labels write above already re-derived the boundary rule's flagged-node
+            # counts for the handle's own flags; only a different rule or flag set needs them
+            # recounted
+            if not same:
+                self.set_accept(rule, fl)
         if "sched_rows" in ck:
             self.set_schedule(ck["sched_rows"], int(ck["sched_t0"]))
         elif "accept_rule" in ck:
@@ -372,11 +388,14 @@ class Chains:
     def from_checkpoint(cls, dgraph: "DeviceGraph", path: str, k: int, proposal=None,
                         pop_bounds=None, percent: float = 0.05) -> "Chains":
         """A new handle resumed from ``save_checkpoint`` output (numpy, no pickle), with the
-        proposal mode, accept rule and bound schedule the checkpointed chains ran under."""
+        proposal mode, population bounds, accept rule and bound schedule the checkpointed
+        chains ran under (``pop_bounds`` / ``percent`` only for checkpoints without bounds)."""
         d = np.load(path, allow_pickle=False)
         labels = d["labels"]
         if proposal is None:
             proposal = int(d["mode"]) if "mode" in d.files else "pairs"
+        if pop_bounds is None and "pop_lo" in d.files:
+            pop_bounds = (int(d["pop_lo"]), int(d["pop_hi"]))
         ch = cls(dgraph, labels.shape[0], k, labels, proposal=proposal, pop_bounds=pop_bounds,
                  percent=percent, seed=int(d["seed"]), chain_id0=int(d["chain_id0"]),
                  thr=d["thr"])

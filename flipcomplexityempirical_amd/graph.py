@@ -295,11 +295,39 @@ def boundary_flags(g: Graph) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- C4 dual graph
+def hilbert_index(xy: np.ndarray, bits: int = 16) -> np.ndarray:
+    """Position of each point of the unit square (rows of ``xy``) along the Hilbert curve of
+    a 2^bits x 2^bits lattice (the classic xy -> d rotation walk, vectorised)."""
+    side = 1 << bits
+    x = np.minimum((xy[:, 0] * side).astype(np.int64), side - 1)
+    y = np.minimum((xy[:, 1] * side).astype(np.int64), side - 1)
+    d = np.zeros(len(xy), np.int64)
+    s = side >> 1
+    while s > 0:
+        rx = (x & s) > 0
+        ry = (y & s) > 0
+        d += s * s * ((3 * rx) ^ ry)
+        # rotate the quadrant so the sub-curve has the canonical orientation
+        flip = ~ry
+        swap_x = np.where(flip & rx, s - 1 - x, x)
+        swap_y = np.where(flip & rx, s - 1 - y, y)
+        x = np.where(flip, swap_y, x)
+        y = np.where(flip, swap_x, y)
+        s >>= 1
+    return d
+
+
 def delaunay_graph(n_points: int = 9000, seed: int = 0, pop_median: float = 1000.0,
-                   pop_sigma: float = 0.8) -> Graph:
+                   pop_sigma: float = 0.8, order: str = "random") -> Graph:
     """Delaunay triangulation of ``n_points`` points drawn by
     ``np.random.default_rng(seed).random((n, 2))``, node populations
-    ``max(1, round(lognormal(ln pop_median, pop_sigma)))`` from the same generator."""
+    ``max(1, round(lognormal(ln pop_median, pop_sigma)))`` from the same generator.
+
+    ``order``: node ids in the points' draw order ("random": unrelated to position), or
+    along the Hilbert curve of the points ("hilbert": the same graph up to isomorphism,
+    numbered so that neighbours get nearby ids, as census units in a shapefile's
+    geographic order do — a node's neighbours then share its 64-node weight group and
+    nearby rows of the padded adjacency table)."""
     from scipy.spatial import Delaunay
     rng = np.random.default_rng(seed)
     pts = rng.random((n_points, 2))
@@ -307,7 +335,15 @@ def delaunay_graph(n_points: int = 9000, seed: int = 0, pop_median: float = 1000
     indptr, indices = tri.vertex_neighbor_vertices
     pop = np.maximum(1, np.rint(rng.lognormal(np.log(pop_median), pop_sigma, n_points))).astype(
         np.int64)
-    nodes = list(range(n_points))
-    adj = {v: indices[indptr[v]:indptr[v + 1]].tolist() for v in nodes}
-    attrs = [{"x": float(pts[v, 0]), "y": float(pts[v, 1])} for v in nodes]
+    if order == "random":
+        key = np.arange(n_points)
+    elif order == "hilbert":
+        key = np.empty(n_points, np.int64)
+        key[np.argsort(hilbert_index(pts), kind="stable")] = np.arange(n_points)
+    else:
+        raise ValueError("order must be 'random' or 'hilbert'")
+    nodes = [int(key[v]) for v in range(n_points)]
+    adj = {int(key[v]): [int(key[u]) for u in indices[indptr[v]:indptr[v + 1]]]
+           for v in range(n_points)}
+    attrs = [{"x": float(pts[v, 0]), "y": float(pts[v, 1])} for v in range(n_points)]
     return Graph.from_adjacency(nodes, adj, pop.tolist(), attrs)

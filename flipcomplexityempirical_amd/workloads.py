@@ -79,7 +79,11 @@ class Workload:
                 f"{', ...' if len(idx) > 8 else ''})")
 
 
-def workload(name: str, grid: Optional[int] = None, k: Optional[int] = None) -> Workload:
+C4_ORDER = "random"  # node numbering of the C4 Delaunay graph (graph.delaunay_graph)
+
+
+def workload(name: str, grid: Optional[int] = None, k: Optional[int] = None,
+             order: Optional[str] = None) -> Workload:
     from .graph import (block_seed, delaunay_graph, frankenstein_graph, frankenstein_seed,
                         grid_graph)
     from .seeds import tree_seed
@@ -91,10 +95,12 @@ def workload(name: str, grid: Optional[int] = None, k: Optional[int] = None) -> 
         return Workload(name, g, init, kk, "pairs", 0.05, 65536 if name == "c3" else 4096, MU,
                         f"{name.upper()}: {n}x{n} grid, k={kk} block seed")
     if name == "c4":
-        g = delaunay_graph(9000, seed=0)
+        order = order or C4_ORDER
+        g = delaunay_graph(9000, seed=0, order=order)
         kk = k or 18
         return Workload(name, g, tree_seed(g, kk, 0.05), kk, "pairs", 0.05, 16384, MU,
-                        f"C4: 9000-node Delaunay dual graph (lognormal pops), k={kk} tree seed")
+                        f"C4: 9000-node Delaunay dual graph (lognormal pops, {order} node "
+                        f"order), k={kk} tree seed")
     if name == "c5":
         n = grid or 200
         g = grid_graph(n, n)

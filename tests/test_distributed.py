@@ -196,3 +196,39 @@ def test_gpu_run_sharded_two_ranks_bit_identical(tmp_path, gpu_lib):
                         base=bases, seed=SEED)
     assert np.array_equal(one.hist_cut, ref.hist_cut) and np.array_equal(one.hist_b, ref.hist_b)
     assert np.array_equal(one.stats.view(np.uint8), ref.stats.view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_bench_under_torchrun_two_ranks(tmp_path, gpu_lib):
+    """bench.py itself under torch.distributed.run at world 2 (gloo process group, both ranks
+    on device 0): the max-over-ranks timing, the checker all-reduce and the histogram merge
+    of the multi-rank path.  Every checked chain equals the oracle, every yield lands in one
+    bin of each merged histogram, and the merged histograms and the final per-chain cut / |B|
+    equal a world-1 run of the same 8,192 chains bit for bit."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = ["--config", "c3", "--chains", "8192", "--steps", "2", "--warmup", "1",
+            "--inner", "300", "--no-cpu-baseline", "--check-chains", "4"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    h2, h1 = str(tmp_path / "w2.npz"), str(tmp_path / "w1.npz")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--backend", "gloo", "--same-device", "--save-hist", h2] + args,
+                       capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    pc = line["parity_check"]
+    assert pc["ranks"] == 2 and pc["equal"] == pc["chains"] >= 8, pc
+    assert pc["hist_yields_equal"]
+    assert line["hist_yields"] == 8192 * (3 * 300 + 1)
+    r1 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--save-hist", h1] + args,
+                        capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    one = json.loads(r1.stdout.strip().splitlines()[-1])
+    assert one["hist_yields"] == line["hist_yields"]
+    a, b = np.load(h2), np.load(h1)
+    for key in ("hist_cut", "hist_b", "final"):
+        assert np.array_equal(a[key], b[key]), key

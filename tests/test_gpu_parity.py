@@ -531,6 +531,26 @@ def test_checkpoint_resume_bit_exact(gpu_lib, name, path, monkeypatch, tmp_path)
     # the resumed run is also the oracle's uninterrupted 700-step run
     _, ost = oracle_chains(case, 71, range(9, 21), [700])[:2]
     assert_stats_equal(ch2.stats(), ost)
+    # the checkpoint carries the population bounds: resuming without them runs the same
+    # chain, and a handle with other bounds refuses it
+    ch3 = Chains.from_checkpoint(dg, path_ck, case.k, proposal=case.mode, percent=0.5)
+    assert (ch3.pop_lo, ch3.pop_hi) == tuple(case.bounds)
+    ch3.run(400)
+    assert ch3.stats().tobytes() == ch2.stats().tobytes()
+    ck = dict(np.load(path_ck, allow_pickle=False))
+    ck["stats"] = ck["stats"].view(ch.stats().dtype)
+    ch4 = Chains(dg, 12, case.k, case.init, proposal=case.mode,
+                 pop_bounds=(case.bounds[0] - 1, case.bounds[1]), base=case.base, seed=71,
+                 chain_id0=9)
+    with pytest.raises(ValueError, match="population bounds"):
+        ch4.restore(ck)
+    # sampled waits on, but a checkpoint without them: refused instead of silently
+    # restarting the sums
+    ch5 = Chains(dg, 12, case.k, case.init, proposal=case.mode, pop_bounds=case.bounds,
+                 base=case.base, seed=71, chain_id0=9)
+    ch5.enable_sampled_waits()
+    with pytest.raises(ValueError, match="sampled waits"):
+        ch5.restore(ck)
 
 
 @pytest.mark.parametrize("name,rule,path", [("grid10_k2_bi", "boundary", "auto"),

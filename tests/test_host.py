@@ -141,3 +141,14 @@ def test_write_wait_txt(tmp_path):
     p = tmp_path / "2B10P5wait.txt"  # grid_chain_sec11.py:410 naming
     write_wait_txt(str(p), w)
     assert p.read_text() == str(int(round(w))) and "\n" not in p.read_text()
+
+
+def test_bench_refuses_maps_with_resume():
+    """bench.py --maps --resume cannot work (plan writes are refused under maps, maps cannot
+    be enabled after a restore): argparse rejects the pair before anything is built."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--maps", "--resume",
+                        "x.npz"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "--maps cannot be combined with --resume" in r.stderr
