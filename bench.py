@@ -219,6 +219,25 @@ def flipwalk_env():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("FLIPWALK_")}
 
 
+# ------------------------------------------------------------------ PMC profiles
+def pmc_key(config, order, chains, inner, steady):
+    """Name of the PMC summary of a workload (profiles/pmc/<key>.json): configuration, chains
+    on this GPU, steps per launch, and whether the chains were resumed at the steady state."""
+    from flipcomplexityempirical_amd.workloads import C4_ORDER
+    name = config
+    if config == "c4" and (order or C4_ORDER) != "random":
+        name += "h"
+    return f"{name}_{chains}_{inner}" + ("_steady" if steady else "")
+
+
+def load_pmc(pmc_dir, key):
+    path = os.path.join(pmc_dir, key + ".json")
+    if not pmc_dir or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
@@ -268,9 +287,10 @@ def main():
     ap.add_argument("--save-hist", default=None, metavar="NPZ",
                     help="rank 0 writes the merged histograms (hist_cut, hist_b) and the "
                          "gathered per-chain final cut / |B| to this file")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
-                    help="per-launch HBM bytes from a rocprofv3 PMC pass of the default C3 "
-                         "command (scripts/profile.sh -> scripts/pmc_summary.py)")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "pmc"),
+                    help="per-workload rocprofv3 PMC summaries (scripts/profile.sh -> "
+                         "scripts/pmc_summary.py), named by pmc_key(): per-launch HBM traffic, "
+                         "VALU issue and achieved occupancy for the roofline fields")
     args = ap.parse_args()
     if args.maps and args.resume:
         # fw_chains_write refuses plan writes while maps are on, and maps cannot be enabled
@@ -393,26 +413,28 @@ def main():
     kernel_ms = float(np.mean(kms))
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic = None
+    prof = load_pmc(args.pmc_dir, pmc_key(args.config, args.order, chains, args.inner,
+                                          bool(args.resume)))
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
     issue = None
-    default_c3 = (args.config, g.n, k, chains, args.inner, proposal) == (
-        "c3", 10000, 4, 65536, 1000, "pairs")
-    if default_c3 and args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        traffic = tj.get("hbm_bytes_per_launch")
-        if tj.get("valu_insts_per_launch"):
-            # what binds this kernel: VALU issue.  Peak: every SIMD takes one wave64 VALU
-            # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md) -> 256 CUs x 4 SIMDs
-            # x 2.4 GHz / 2; achieved: the PMC pass's VALU wave-instructions per launch
-            # over this run's mean launch time.
-            peak = 256 * 4 * 2.4e9 / 2
-            ach = tj["valu_insts_per_launch"] / (kernel_ms * 1e-3)
-            issue = {"bound": "valu-issue", "achieved": ach, "peak": peak,
-                     "unit": "wave-instr/s", "frac": ach / peak,
-                     "source": tj.get("source"),
-                     # rocprofv3 --kernel-trace --stats mean of the same kernel, same command
-                     "rocprof_kernel_ms": (tj.get("kernel_trace") or {}).get("avg_ms")}
+    if prof and prof.get("valu_insts_per_launch"):
+        # what binds this kernel: VALU issue.  Peak: every SIMD takes one wave64 VALU
+        # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md) -> 256 CUs x 4 SIMDs
+        # x 2.4 GHz / 2; achieved: the PMC pass's VALU wave-instructions per launch
+        # over this run's mean launch time.
+        peak = 256 * 4 * 2.4e9 / 2
+        ach = prof["valu_insts_per_launch"] / (kernel_ms * 1e-3)
+        issue = {"bound": "valu-issue", "achieved": ach, "peak": peak,
+                 "unit": "wave-instr/s", "frac": ach / peak, "source": prof.get("source"),
+                 # rocprofv3 --kernel-trace --stats mean of the same kernel, same command
+                 "rocprof_kernel_ms": (prof.get("kernel_trace") or {}).get("avg_ms")}
+    occupancy = dict(ch.launch_info())
+    occupancy["achieved_waves_per_simd"] = prof.get("achieved_waves_per_simd") if prof else None
+    occupancy["source"] = prof.get("source") if prof else None
+    l2 = None
+    if prof and prof.get("l2_requests_per_launch") is not None:
+        l2 = {"requests_per_launch": prof["l2_requests_per_launch"], "hit": prof.get("l2_hit"),
+              "requests_per_attempt": prof["l2_requests_per_launch"] / max(1.0, d["attempts"] / args.steps)}
 
     if rank == 0:
         if args.shard:
@@ -465,6 +487,8 @@ def main():
                 "traffic": traffic,
             },
             "issue_roofline": issue,
+            "occupancy": occupancy,
+            "l2": l2,
             "kernel_ms": kernel_ms,
             "proposals_per_s": att_all / dt,
             "accepts_per_s": acc_all / dt,

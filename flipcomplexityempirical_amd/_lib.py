@@ -65,6 +65,7 @@ SIGNATURES = [
     ("fw_chains_sync", ctypes.c_int, [_P]),
     ("fw_chains_run_traced", ctypes.c_int, [_P, _I64, _I32, _P, ctypes.c_size_t]),
     ("fw_chains_last_kernel_ms", ctypes.c_double, [_P]),
+    ("fw_chains_launch_info", ctypes.c_int, [_P, _P]),
     ("fw_chains_read", ctypes.c_int, [_P, _I32, _P, ctypes.c_size_t]),
     ("fw_chains_write", ctypes.c_int, [_P, _I32, _P, ctypes.c_size_t]),
     ("fw_chains_reset_observables", ctypes.c_int, [_P]),

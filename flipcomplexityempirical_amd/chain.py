@@ -212,6 +212,20 @@ class Chains:
     def last_kernel_ms(self) -> float:
         return float(_lib.load().fw_chains_last_kernel_ms(self._h))
 
+    def launch_info(self) -> dict:
+        """The launch plan (fw_chains_launch_info) and the residency it gives: waves per SIMD
+        and chains per CU of the persistent grid (4 SIMDs per CU)."""
+        info = np.zeros(8, np.int64)
+        check(_lib.load().fw_chains_launch_info(self._h, ptr(info)))
+        wgs, nw, cpw, lds, vgpr, scratch, cus, per_cu = (int(x) for x in info)
+        resident = min(wgs, per_cu * cus)
+        return {"workgroups": wgs, "waves_per_workgroup": nw, "chains_per_wave": cpw,
+                "lds_bytes_per_workgroup": lds, "vgprs": vgpr, "scratch_bytes_per_lane": scratch,
+                "cus": cus, "workgroups_per_cu": per_cu,
+                "waves_per_simd_limit": per_cu * nw / 4.0,
+                "waves_per_simd": resident * nw / (4.0 * cus),
+                "chains_per_cu": resident * nw * cpw / cus}
+
     def reset_observables(self) -> None:
         check(_lib.load().fw_chains_reset_observables(self._h))
 

@@ -284,7 +284,7 @@ extern "C" {
 
 const char* fw_last_error(void) { return g_err.c_str(); }
 
-int32_t fw_version(void) { return 0x000500; }
+int32_t fw_version(void) { return 0x000600; }
 
 int32_t fw_device_count(void) {
   int c = 0;
@@ -804,6 +804,32 @@ double fw_chains_last_kernel_ms(const fw_chains* c) {
   float ms = -1.f;
   if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0;
   return ms;
+}
+
+int fw_chains_launch_info(const fw_chains* c, int64_t info[8]) {
+  if (!c || !info) return fail(FW_EINVAL, "fw_chains_launch_info: null");
+  HIPCHK(hipSetDevice(c->g->device));
+  const FwRunParams& p = c->p;
+  void* fn = p.use16 ? fw_grid16_fn(p) : fw_run_fn(p, c->lb);
+  if (!fn) return fail(FW_EHIP, "no kernel for this plan");
+  hipFuncAttributes at;
+  HIPCHK(hipFuncGetAttributes(&at, fn));
+  const int nw = p.use16 ? fw_grid16_launch_nw(p) : 1;
+  const int lds = p.use16 ? p.lds16 : p.lds_bytes;
+  int per_cu = 0;
+  HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nw, (size_t)lds));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, c->g->device));
+  info[0] = c->grid;
+  info[1] = nw;
+  info[2] = p.use16 ? 4 / fw_grid16_launch_rows(p) : 1;
+  info[3] = lds;
+  info[4] = at.numRegs;
+  info[5] = (int64_t)at.localSizeBytes;
+  info[6] = prop.multiProcessorCount;
+  info[7] = per_cu;
+  return FW_OK;
 }
 
 int fw_chains_read(fw_chains* c, int32_t what, void* host_dst, size_t bytes) {

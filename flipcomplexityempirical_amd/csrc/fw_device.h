@@ -569,11 +569,16 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
 }
 
 // Where grid_race_bb2's two-class race stopped when its frontier reached the window edge:
-// per lane (grid row vr - 32 + lane, columns vc - 32 ...) the cells each class has visited
-// and its current frontier, and the direction that represents each class.  The list search
-// continues the race from here instead of from the sources (race_search_b3).
+// per lane (grid row vr - 32 + lane, columns vc - 32 ...) each class's current frontier
+// (level L) and previous one (level L - 1), the count and degree sum of the cells already
+// processed (levels < L), and the direction that represents each class.  The list search
+// continues the race from here instead of from the sources (race_search_b3).  Only levels
+// L - 1 and L need marks: the race is a breadth-first search of (district a) minus v, so a
+// neighbour of a level-L cell lies at level L - 1, L or L + 1, and the cells of levels
+// < L - 1 are never met again.
 struct BBSeed {
-  uint32_t va0, va1, vb0, vb1, fa0, fa1, fb0, fb1;
+  uint32_t qa0, qa1, qb0, qb1, fa0, fa1, fb0, fb1;
+  uint32_t pc, pdeg;  // processed cells of this lane's row, their degree sum
   int ra, rb;  // representative directions (0 up, 1 left, 2 right, 3 down)
   bool ok;
 };
@@ -658,12 +663,20 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
         Fb1 |= b1;
       }
     }
-    uint32_t Va0 = Fa0, Va1 = Fa1, Vb0 = Fb0, Vb1 = Fb1;  // visited, per class
+    uint32_t Qa0 = 0u, Qa1 = 0u, Qb0 = 0u, Qb1 = 0u;  // the previous level, per class
     uint32_t V0 = Fa0 | Fb0, V1 = Fa1 | Fb1;
     int vd;
     for (;;) {
       if (ballot((((Fa0 | Fb0) & E0) | ((Fa1 | Fb1) & E1)) != 0u)) {
-        sd = BBSeed{Va0, Va1, Vb0, Vb1, Fa0, Fa1, Fb0, Fb1, ra, rb, true};
+        // processed cells (levels < L) and their degrees, counted as the list search counts
+        // its dequeued nodes
+        const uint32_t P0 = V0 & ~(Fa0 | Fb0), P1 = V1 & ~(Fa1 | Fb1);
+        const uint32_t pc = (uint32_t)(__popc(P0) + __popc(P1));
+        uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
+        auto pbit = [&](int pos) { return pos < 32 ? (P0 >> pos) & 1u : (P1 >> (pos - 32)) & 1u; };
+        if (c0 <= 0) dg -= pbit(-c0);
+        if (W - c0 <= 64) dg -= pbit(W - c0 - 1);
+        sd = BBSeed{Qa0, Qa1, Qb0, Qb1, Fa0, Fa1, Fb0, Fb1, pc, dg, ra, rb, true};
         return -1;
       }
       const uint32_t Da0 = (Fa0 | (Fa0 << 1) | (Fa0 >> 1) | (Fa1 << 31) | from_prev_lane(Fa0) | from_next_lane(Fa0)) & A0;
@@ -675,6 +688,10 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
         vd = 1;  // the two classes met: connected, the cells processed are V
         break;
       }
+      Qa0 = Fa0;
+      Qa1 = Fa1;
+      Qb0 = Fb0;
+      Qb1 = Fb1;
       Fa0 = Da0 & nw0;
       Fa1 = Da1 & nw1;
       Fb0 = Db0 & nw0;
@@ -685,10 +702,6 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
       }
       V0 |= nw0;
       V1 |= nw1;
-      Va0 |= Fa0;
-      Va1 |= Fa1;
-      Vb0 |= Fb0;
-      Vb1 |= Fb1;
     }
     const uint32_t pc = (uint32_t)(__popc(V0) + __popc(V1));
     uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
@@ -1267,30 +1280,27 @@ struct Ctx {
   // memory-side atomics (global atomics execute past the XCD's L2).  A claimed node's label
   // a becomes its class's code: the unused labels k..7 first, then district labels absent
   // from a 256-cell sample around v.  A borrowed code is ambiguous (a cell of that district,
-  // or a visited one), so claims under it also set the node's byte in an HBM map (n bytes
-  // per workgroup, plain byte stores), read (L2-served sc1 loads, after the stores drained)
-  // only when a frontier node of another, unmerged class meets the code: the merge test.
-  // Within a level the four neighbour directions run one after another, so a node claimed
-  // in an earlier direction reads as claimed (LDS ops of one wave execute in program order)
-  // and no node is pushed twice: on a grid two frontier nodes reach the same node in one
-  // direction only if they are the same node.  A list entry carries its class (node |
-  // class << 16).  The next level is staged in LDS over the chain's group sums (not read
-  // while the search runs; up to scap entries, the displaced words held in two VGPRs) and
-  // every entry goes to the HBM visit list, from which a larger level is read and the
-  // labels and map bytes are restored at the end.  With a seed (grid_race_bb2's two-class
-  // race left its 64 x 64 window), the race continues from the bitboard's visited cells and
-  // frontier instead of from the sources.
+  // or a visited one): when a frontier node of one class meets the code of another, unmerged
+  // class (the merge test), the node is looked up among the entries of the current level
+  // and of the next level so far.  That is complete: the race is breadth-first, so a visited
+  // neighbour of a level-L node lies at level L - 1, L or L + 1, and one of another class at
+  // level L - 1 would already have merged the two classes.  Within a level the four
+  // neighbour directions run one after another, so a node claimed in an earlier direction
+  // reads as claimed (LDS ops of one wave execute in program order) and no node is pushed
+  // twice: on a grid two frontier nodes reach the same node in one direction only if they
+  // are the same node.  A list entry carries its class (node | class << 16).  The next level
+  // is staged in LDS over the chain's group sums (not read while the search runs; up to scap
+  // entries, the displaced words held in two VGPRs); every entry also goes to the HBM visit
+  // list (coalesced 4-byte stores), from which a larger level is read and the labels are
+  // restored at the end.  With a seed (grid_race_bb2's two-class race left its 64 x 64
+  // window), the race continues from the bitboard's last two levels instead of from the
+  // sources.
   __device__ bool race_search_b3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
                                  const BBSeed& sd, uint64_t& bfs_nodes, uint64_t& bfs_deg) {
     LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
-    // the map: one byte per node, set and cleared by plain byte stores (global atomics
-    // execute past the XCD's L2 and drop the line), read by L2-served sc1 loads after the
-    // stores have drained
-    GLB uint32_t* const bm = gscr;
-    GLB uint8_t* const bmap = reinterpret_cast<GLB uint8_t*>(gscr);
     // class codes: unused labels first, then borrowed ones, preferring district labels
     // absent from a sample of 256 cells around v (a 16 x 16 lattice of step 4): a code
-    // met by a frontier is then rarely a real district cell, so map tests stay rare
+    // met by a frontier is then rarely a real district cell, so merge tests stay rare
     uint32_t codes = 0, ambig = 0;  // 3-bit code of class o at bits 3o; ambiguous: bit o
     {
       int vr, vc;
@@ -1337,27 +1347,56 @@ struct Ctx {
     int lb = 0, le = m;
     uint32_t my_deg = 0;
     uint64_t nodes = 0;
+    // the merge test of an ambiguous code: is y (held by the lanes of `want`) an entry of the
+    // current level [lb, le) (in q0 / q1 when the level is staged) or of the next level so
+    // far [le, le + nn) (its first scap entries in the stage)?  Rare (a code absent from the
+    // sample met far from v), so the lanes are served one at a time.
+    auto listed = [&](uint64_t want, int y, int cnt, bool staged, uint32_t q0, uint32_t q1,
+                      int nn) -> bool {
+      const int ns = nn < scap ? nn : scap;
+      const uint32_t s0 = lane < ns ? stage[lane] : 0u;
+      const uint32_t s1 = lane + WAVE < ns ? stage[lane + WAVE] : 0u;
+      const bool hbm = !staged || nn > scap;
+      const int h0 = staged ? le + scap : lb, h1 = le + nn;  // entries read from the HBM list
+      if (hbm) __threadfence_block();  // this level's spilled entries are read back
+      bool hit = false;
+      while (want) {
+        const int Lr = __ffsll((unsigned long long)want) - 1;
+        want &= want - 1;
+        const uint32_t yy = (uint32_t)rdl((int32_t)y, Lr);
+        bool f = (lane < ns && (s0 & 0xFFFFu) == yy) || (lane + WAVE < ns && (s1 & 0xFFFFu) == yy);
+        if (staged)
+          f = f || (lane < cnt && (q0 & 0xFFFFu) == yy) || (lane + WAVE < cnt && (q1 & 0xFFFFu) == yy);
+        if (hbm) {
+          for (int b = h0; b < h1; b += WAVE) {
+            const int i = b + lane;
+            uint32_t e = 0u;
+            if (i < h1) e = spill[i];
+            f = f || (i < h1 && (e & 0xFFFFu) == yy);
+          }
+        }
+        if (ballot(f)) hit = hit || lane == Lr;
+      }
+      return hit;
+    };
     if (sd.ok) {
-      // continue grid_race_bb2's race where it left its window: its visited cells take
-      // their class's code and form the head of the visit list (the processed cells, counted
-      // as the bitboard counts them), its frontier the current level
+      // continue grid_race_bb2's race where it left its window: its last two levels take
+      // their class's code and form the head of the visit list (the previous level, then
+      // the current one); the cells processed before are never met again and are counted
+      // as the bitboard counts them
 #ifdef FW_STAMPS
       n_seed += 1;
 #endif
       int vr, vc;
       divmod(v, vr, vc);
       const int r = vr - 32 + lane, c0 = vc - 32;
-      const uint32_t pa0 = sd.va0 & ~sd.fa0, pa1 = sd.va1 & ~sd.fa1;
-      const uint32_t pb0 = sd.vb0 & ~sd.fb0, pb1 = sd.vb1 & ~sd.fb1;
-      const uint32_t c1 = (uint32_t)(__popc(pa0) + __popc(pa1) + __popc(pb0) + __popc(pb1));
+      const uint32_t c1 = (uint32_t)(__popc(sd.qa0) + __popc(sd.qa1) + __popc(sd.qb0) + __popc(sd.qb1));
       const uint32_t c2 = (uint32_t)(__popc(sd.fa0) + __popc(sd.fa1) + __popc(sd.fb0) + __popc(sd.fb1));
       const uint32_t i1 = scan_incl(c1), i2 = scan_incl(c2);
       const int n1 = (int)rdl(i1, 63), n2 = (int)rdl(i2, 63);
       const uint32_t ca = (codes >> (3 * sd.ra)) & 7u, cb = (codes >> (3 * sd.rb)) & 7u;
-      const bool ma = (ambig >> sd.ra) & 1u, mb = (ambig >> sd.rb) & 1u;
       // one class's cells of one dword of this lane's row, from list index idx on
-      auto emit = [&](uint32_t bits, int col, uint32_t o, uint32_t code, bool amb, int& idx,
-                      bool staged) {
+      auto emit = [&](uint32_t bits, int col, uint32_t o, uint32_t code, int& idx, bool staged) {
         while (bits) {
           const int t = __ffs(bits) - 1;
           bits &= bits - 1;
@@ -1366,35 +1405,28 @@ struct Ctx {
           spill[idx] = e;
           if (staged && idx - n1 < scap) stage[idx - n1] = e;
           P::axor(lab, x, a ^ code);
-          if (amb) bmap[x] = 1u;
           ++idx;
         }
       };
       int idx = (int)(i1 - c1);
-      emit(pa0, c0, (uint32_t)sd.ra, ca, ma, idx, false);
-      emit(pa1, c0 + 32, (uint32_t)sd.ra, ca, ma, idx, false);
-      emit(pb0, c0, (uint32_t)sd.rb, cb, mb, idx, false);
-      emit(pb1, c0 + 32, (uint32_t)sd.rb, cb, mb, idx, false);
+      emit(sd.qa0, c0, (uint32_t)sd.ra, ca, idx, false);
+      emit(sd.qa1, c0 + 32, (uint32_t)sd.ra, ca, idx, false);
+      emit(sd.qb0, c0, (uint32_t)sd.rb, cb, idx, false);
+      emit(sd.qb1, c0 + 32, (uint32_t)sd.rb, cb, idx, false);
       idx = n1 + (int)(i2 - c2);
-      emit(sd.fa0, c0, (uint32_t)sd.ra, ca, ma, idx, true);
-      emit(sd.fa1, c0 + 32, (uint32_t)sd.ra, ca, ma, idx, true);
-      emit(sd.fb0, c0, (uint32_t)sd.rb, cb, mb, idx, true);
-      emit(sd.fb1, c0 + 32, (uint32_t)sd.rb, cb, mb, idx, true);
+      emit(sd.fa0, c0, (uint32_t)sd.ra, ca, idx, true);
+      emit(sd.fa1, c0 + 32, (uint32_t)sd.ra, ca, idx, true);
+      emit(sd.fb0, c0, (uint32_t)sd.rb, cb, idx, true);
+      emit(sd.fb1, c0 + 32, (uint32_t)sd.rb, cb, idx, true);
       // the bitboard's counters over the processed cells (grid_race_bb2)
-      const uint32_t q0 = pa0 | pb0, q1 = pa1 | pb1;
-      uint32_t dg = c1 * (uint32_t)((r > 0) + (r < g.gh - 1) + 2);
-      auto qbit = [&](int pos) { return pos < 32 ? (q0 >> pos) & 1u : (q1 >> (pos - 32)) & 1u; };
-      if (c0 <= 0) dg -= qbit(-c0);
-      if (g.gw - c0 <= 64) dg -= qbit(g.gw - c0 - 1);
-      my_deg += dg;
-      nodes += (uint64_t)n1;
+      my_deg += sd.pdeg;
+      nodes += (uint64_t)wave_sum(sd.pc);
       lb = n1;
       le = n1 + n2;
       if (n2 > scap) __threadfence_block();  // the level is read from the HBM list
     } else if (lane < m) {
       const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
       P::axor(lab, src, a ^ ((codes >> (3 * lane)) & 7u));
-      if ((ambig >> lane) & 1u) bmap[src] = 1u;
       spill[lane] = e;
       stage[lane] = e;
     }
@@ -1428,7 +1460,7 @@ struct Ctx {
           const uint32_t o = e >> 16;
           const bool isa = o == oa;
           const uint32_t co = isa ? ca : cb, cother = isa ? cb : ca;
-          const bool amb_o = isa ? ma : mb, amb_other = isa ? mb : ma;
+          const bool amb_other = isa ? mb : ma;
           int xr = 0, xc = 0;
           divmod(x, xr, xc);
           if (act) my_deg += (uint32_t)degree(x, xr, xc);
@@ -1447,7 +1479,6 @@ struct Ctx {
             const uint64_t pm = ballot(push);
             if (pm) {
               if (push) {
-                if (amb_o) bmap[y] = 1u;
                 const int slot = nn + (int)mbcnt(pm);
                 const uint32_t ent = (uint32_t)y | (o << 16);
                 spill[le + slot] = ent;
@@ -1461,17 +1492,17 @@ struct Ctx {
             if (oth && amb_other) chk |= 1u << j;
           }
           merged |= ballot(met) != 0ull;
-          if (!merged && ballot(chk != 0u)) {  // map tests after this chunk's stores drained
+          if (!merged && ballot(chk != 0u)) {  // merge tests of ambiguous codes
 #ifdef FW_STAMPS
             n_mapt += 1;
 #endif
-            __threadfence_block();
+            lds_order();
             bool hit = false;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if ((chk >> j) & 1u)
-                hit |= ((__hip_atomic_load(bm + (ys[j] >> 2), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT) >> ((ys[j] & 3) << 3)) & 0xFFu) != 0u;
+            for (int j = 0; j < 4; ++j) {
+              const uint64_t want = ballot((chk >> j) & 1u);
+              if (want) hit |= listed(want, ys[j], cnt, staged, q0, q1, nn);
+            }
             merged |= ballot(hit) != 0ull;
           }
           pa |= ballot(pushed && isa) != 0ull;
@@ -1520,7 +1551,6 @@ struct Ctx {
         const int x = (int)(e & 0xFFFFu);
         const uint32_t o = e >> 16;
         const uint32_t co = (codes >> (3 * o)) & 7u;
-        const bool amb_o = (ambig >> o) & 1u;
         int xr = 0, xc = 0;
         divmod(x, xr, xc);
         if (act) my_deg += (uint32_t)degree(x, xr, xc);
@@ -1540,7 +1570,6 @@ struct Ctx {
           const uint64_t pm = ballot(push);
           if (pm) {
             if (push) {
-              if (amb_o) bmap[y] = 1u;
               const int slot = nn + (int)mbcnt(pm);
               const uint32_t ent = (uint32_t)y | (o << 16);
               spill[le + slot] = ent;
@@ -1550,7 +1579,7 @@ struct Ctx {
           }
           pushed |= push;
           // a class code of another class not yet merged with this one: a merge if the
-          // node is a visited one (certain for unused-label codes, a map test otherwise)
+          // node is a visited one (certain for unused-label codes, a list lookup otherwise)
           const uint32_t c1 = ok && !push ? (cls_of >> (3 * ly)) & 7u : 0u;
           const bool other = c1 != 0u && ((M >> (4 * o + (c1 - 1u))) & 1u) == 0u;
           const bool sure = other && !((ambig >> (c1 - 1u)) & 1u);
@@ -1565,19 +1594,16 @@ struct Ctx {
             unite(rdl((int32_t)o, Lr), rdl((int32_t)(c1 - 1u), Lr));
           }
         }
-        if (ballot(chk != 0u)) {  // the map tests of this chunk, after its claims landed
+        if (ballot(chk != 0u)) {  // the merge tests of this chunk, after its claims
 #ifdef FW_STAMPS
           n_mapt += 1;
 #endif
-          __threadfence_block();
-          uint32_t w[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            w[j] = ((chk >> j) & 1u) ? __hip_atomic_load(bm + (ys[j] >> 2), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT) : 0u;
+          lds_order();
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const bool hit = ((chk >> j) & 1u) && ((w[j] >> ((ys[j] & 3) << 3)) & 0xFFu);
+            const uint64_t want = ballot((chk >> j) & 1u);
+            if (!want) continue;
+            const bool hit = listed(want, ys[j], cnt, staged, q0, q1, nn);
             uint64_t rm = ballot(hit);
             while (rm) {
               const int Lr = __ffsll((unsigned long long)rm) - 1;
@@ -1615,19 +1641,18 @@ struct Ctx {
     const uint64_t t_cl = now();
 #endif
     __threadfence_block();  // the visit list is read back
-    for (int base = 0; base < le; base += WAVE) {  // restore the labels, clear the map
+    for (int base = 0; base < le; base += WAVE) {  // restore the labels
       const int idx = base + lane;
       if (idx < le) {
         const uint32_t e = spill[idx];
         const int x = (int)(e & 0xFFFFu);
         const uint32_t o = e >> 16;
         P::axor(lab, x, a ^ ((codes >> (3 * o)) & 7u));
-        if ((ambig >> o) & 1u) bmap[x] = 0u;
       }
     }
     if (lane < scap) stage[lane] = sv0;
     if (lane + WAVE < scap) stage[lane + WAVE] = sv1;
-    __threadfence_block();
+    lds_order();
 #ifdef FW_STAMPS
     c_clear += now() - t_cl;
 #endif

@@ -168,6 +168,9 @@ int fw_run_gsum_slots(int G);  // u16 group-sum slots of the chain kernel
 bool fw_grid16_candidate(int gw, int maxdeg, int G, int k, int64_t total_pop);
 int fw_grid16_lb(int G, int k);
 void* fw_grid16_fn(const FwRunParams& p);
+void* fw_run_fn(const FwRunParams& p, int lb);  // the chain-kernel instantiation fw_launch_run takes
+int fw_grid16_launch_nw(const FwRunParams& p);
+int fw_grid16_launch_rows(const FwRunParams& p);
 int fw_grid16_plan(FwRunParams& p, int device, int* grid);
 int fw_grid16_launch(const FwRunParams& p, int grid, void* stream);
 int fw_grid16_launch_rows(const FwRunParams& p);  // rows per chain of the kernel launched

@@ -742,11 +742,15 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   return 0;
 }
 
-int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
-  if (p.use16) return fw_grid16_launch(p, grid, stream);
+void* fw_run_fn(const FwRunParams& p, int lb) {
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
                     p.ring_n > 0 || p.trace != nullptr || p.wsamp != nullptr;
-  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0, full);
+  return pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0, full);
+}
+
+int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
+  if (p.use16) return fw_grid16_launch(p, grid, stream);
+  void* fn = fw_run_fn(p, lb);
   // handles of different graphs share instantiations: set this handle's LDS size
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   if (e != hipSuccess) return (int)e;

@@ -150,8 +150,9 @@ typedef struct fw_chains fw_chains;
 /* Thread-local description of the last error on this thread. */
 const char* fw_last_error(void);
 
-/* Library/ABI version, e.g. 0x000500 for 0.5.0 (0.2: spatial maps; 0.3: bound
- * schedules; 0.4: ring observable, checkpoint/resume; 0.5: sampled geometric waits). */
+/* Library/ABI version, e.g. 0x000600 for 0.6.0 (0.2: spatial maps; 0.3: bound
+ * schedules; 0.4: ring observable, checkpoint/resume; 0.5: sampled geometric waits;
+ * 0.6: fw_chains_launch_info). */
 int32_t fw_version(void);
 
 /* Number of visible HIP devices (0 when none; never fails). */
@@ -197,6 +198,14 @@ int fw_chains_run(fw_chains* c, int64_t steps, int32_t max_retries);
 int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries);
 int fw_chains_sync(fw_chains* c);
 double fw_chains_last_kernel_ms(const fw_chains* c);
+
+/* The launch plan of the handle's next fw_chains_run (no reference counterpart: the
+ * occupancy figures SURVEY.md §8d asks the measurement to report).
+ *  info[0] workgroups of the persistent grid     info[1] waves per workgroup
+ *  info[2] chains per wave                       info[3] LDS bytes per workgroup
+ *  info[4] VGPRs per lane of the kernel           info[5] scratch (spill) bytes per lane
+ *  info[6] compute units of the device           info[7] workgroups resident per CU */
+int fw_chains_launch_info(const fw_chains* c, int64_t info[8]);
 
 /* fw_chains_run plus a per-step trace: host_trace [n_chains][steps] receives, for
  * each counted step, v*64 + target when the flip was accepted, -1 when the

@@ -6,6 +6,7 @@
 # runs the named tasks in order, output under gpurun_out/OUT/, each GPU step under its own
 # time limit, stopping at the first failure.  Tasks:
 #   tests                 every -m gpu test
+#   tests:EXPR            the -m gpu tests selected by -k EXPR (',' for ' ')
 #   smoke                 __graft_entry__.smoke()
 #   bench[:ARGS]          one bench.py line (ARGS with ',' for ' ') -> OUT/bench.jsonl
 #   ck_c5                 C5 shard 0/8 advanced 10^5 steps, checkpoint /tmp/ck_c5_100k.npz
@@ -42,6 +43,13 @@ run_task() {
       grep -E "passed|failed" $O/pytest_gpu.log | tail -2
       grep -E "FAILED|^E " $O/pytest_gpu.log | head -20
       return $rc ;;
+    tests:*)
+      local expr=${t#tests:}; expr=${expr//,/ }
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "$expr" > $O/pytest_gpu_k.log 2>&1
+      local rc=$?
+      grep -E "passed|failed" $O/pytest_gpu_k.log | tail -2
+      grep -E "FAILED|^E " $O/pytest_gpu_k.log | head -20
+      return $rc ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; return 1; }
       tail -2 $O/smoke.log ;;
@@ -55,13 +63,20 @@ run_task() {
       line $O/ck_c5.json ck_c5 ;;
     prof_c5)
       prof c5steady "--config c5 --shard 0/8 --resume $CK5 --check-chains 0" "--steps 5 --warmup 0 --inner 1000 --no-cpu-baseline --config c5 --shard 0/8 --resume $CK5 --check-chains 0" ;;
+    prof_c5:*)  # the same with the library ab/lib_<LIB>.so
+      local lib=${t#prof_c5:}
+      FLIPWALK_LIB=$PWD/ab/lib_$lib.so prof c5steady_$lib "--config c5 --shard 0/8 --resume $CK5 --check-chains 0" "--steps 5 --warmup 0 --inner 1000 --no-cpu-baseline --config c5 --shard 0/8 --resume $CK5 --check-chains 0" ;;
     prof_c4) prof c4 "--config c4" ;;
+    prof_c4h) prof c4h "--config c4 --order hilbert" ;;
     prof_c3) prof c3 "" ;;
     prof_c2) prof c2 "--config c2" ;;
     prof_c3s8) prof c3s8 "--config c3 --shard 0/8" ;;
     stamps_c5)
       timeout -k 10 300 python -u scripts/stamps.py c5 8192 1 $CK5 > $O/stamps_c5_100k.txt 2>&1 || { tail -5 $O/stamps_c5_100k.txt; return 1; }
       grep -v amdgpu.ids $O/stamps_c5_100k.txt ;;
+    stamps_c4h)
+      timeout -k 10 300 python -u scripts/stamps.py c4h 16384 2 > $O/stamps_c4h.txt 2>&1 || { tail -5 $O/stamps_c4h.txt; return 1; }
+      grep -v amdgpu.ids $O/stamps_c4h.txt ;;
     stamps_c4)
       timeout -k 10 300 python -u scripts/stamps.py c4 16384 2 > $O/stamps_c4.txt 2>&1 || { tail -5 $O/stamps_c4.txt; return 1; }
       grep -v amdgpu.ids $O/stamps_c4.txt ;;

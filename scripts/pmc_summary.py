@@ -44,6 +44,17 @@ if len(sys.argv) > 2 and "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
            # issue roofline: wave-instructions, SQ_INSTS_* summed over the chip
            "valu_insts_per_launch": _mean("SQ_INSTS_VALU"), "salu_insts_per_launch": _mean("SQ_INSTS_SALU"),
            "lds_insts_per_launch": _mean("SQ_INSTS_LDS"), "waves": _mean("SQ_WAVES"),
+           # achieved residency: SQ_WAVE_CYCLES counts wave-lifetime in units of 4 cycles
+           # (calibrated on the C3 grid kernel, whose 3 waves per SIMD live the whole launch:
+           # 2.47e10 x 4 / 3.31e7 cycles / 1024 SIMDs = 2.92), GRBM_GUI_ACTIVE the launch's
+           # busy cycles summed over the 8 XCDs; 256 CUs x 4 SIMDs
+           "achieved_waves_per_simd": (4.0 * _mean("SQ_WAVE_CYCLES") / (_mean("GRBM_GUI_ACTIVE") / 8.0)
+                                       / 1024.0) if _mean("SQ_WAVE_CYCLES") and _mean("GRBM_GUI_ACTIVE") else None,
+           "l2_hit": (_mean("TCC_HIT_sum") / (_mean("TCC_HIT_sum") + _mean("TCC_MISS_sum"))
+                      if _mean("TCC_HIT_sum") is not None and _mean("TCC_MISS_sum") else None),
+           "l2_requests_per_launch": (_mean("TCC_HIT_sum") + _mean("TCC_MISS_sum")
+                                      if _mean("TCC_HIT_sum") is not None and _mean("TCC_MISS_sum") is not None else None),
+           "bench_args": os.environ.get("PMC_BENCH_ARGS"),
            "note": "FETCH_SIZE x2 (gfx950 coalesced-read correction) + WRITE_SIZE, KB->B"}
     with open(sys.argv[2], "w") as f:
         json.dump(out, f, indent=1)

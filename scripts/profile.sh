@@ -21,4 +21,4 @@ for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   timeout -s KILL 150 rocprofv3 --pmc $CTRS -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $PB > $OUT/pmc${i}_bench.log 2>&1 || { echo "pmc pass $i failed rc=$?"; tail -5 $OUT/pmc${i}_bench.log; exit 1; }
   echo "pmc pass $i ok"
 done
-python3 scripts/pmc_summary.py $OUT $OUT/traffic_c3.json > $OUT/summary.txt && cat $OUT/summary.txt
+PMC_BENCH_ARGS="$PB" python3 scripts/pmc_summary.py $OUT $OUT/pmc.json > $OUT/summary.txt && cat $OUT/summary.txt

@@ -31,7 +31,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_version_and_device_count_without_gpu():
     L = _lib.load()
-    assert L.fw_version() == 0x000500
+    assert L.fw_version() == 0x000600
     assert L.fw_device_count() >= 0
 
 
