@@ -428,7 +428,10 @@ def main():
                  "unit": "wave-instr/s", "frac": ach / peak, "source": prof.get("source"),
                  # rocprofv3 --kernel-trace --stats mean of the same kernel, same command
                  "rocprof_kernel_ms": (prof.get("kernel_trace") or {}).get("avg_ms")}
-    occupancy = dict(ch.launch_info())
+    try:
+        occupancy = dict(ch.launch_info())
+    except AttributeError:  # an A/B library older than fw_chains_launch_info
+        occupancy = {}
     occupancy["achieved_waves_per_simd"] = prof.get("achieved_waves_per_simd") if prof else None
     occupancy["source"] = prof.get("source") if prof else None
     l2 = None

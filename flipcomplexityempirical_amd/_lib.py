@@ -115,7 +115,14 @@ def load(path: str = LIB_PATH):
             pass
         L = ctypes.CDLL(path)
         for name, res, args in SIGNATURES:
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                # an older build pointed at by FLIPWALK_LIB (A/B runs) may predate an entry
+                # point; the in-tree library must export them all
+                if path == os.path.join(_HERE, "libflipwalk.so"):
+                    raise
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = L

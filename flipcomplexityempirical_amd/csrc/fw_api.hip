@@ -525,8 +525,9 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     // forbids (5 also for k <= 15).
     if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 && lb == 8 && want == 0) {
       const long long gs = round16((int64_t)fw_run_gsum_slots(G) * 2), lds = 160 * 1024;
-      const long long l8 = round16(((int64_t)n * 8 + 7) / 8 + 8) + gs + 4 * 128;
-      const long long l5 = round16(((int64_t)n * 5 + 7) / 8 + 8) + gs + 4 * 8;
+      const long long wbytes = proposal_mode != FW_PROPOSE_CUTEDGE ? round16(((int64_t)n * 2 + 7) / 8) : 0;
+      const long long l8 = round16(((int64_t)n * 8 + 7) / 8 + 8) + gs + 4 * 128 + wbytes;
+      const long long l5 = round16(((int64_t)n * 5 + 7) / 8 + 8) + gs + 4 * 8 + wbytes;
       if (n > 16384 || std::min(20ll, lds / l5) > std::min(16ll, lds / l8)) lb = 5;
     }
     if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 && want == 5) lb = 5;
@@ -558,7 +559,18 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   }
   // +8: the grid kernels read label dwords one past the last node
   p.lab_bytes = round16(((int64_t)n * lb + 7) / 8 + 8);
-  p.off_gsum = p.lab_bytes;
+  // chain kernel on padded rows with pairs proposals: 2-bit per-node weights in LDS, so the
+  // select reads a group's weights instead of walking its 64 padded rows in L2
+  // (FLIPWALK_NO_WB=1: recompute them from the rows, as before)
+  {
+    const char* e = getenv("FLIPWALK_NO_WB");
+    p.wb = !use16 && g->gw == 0 && g->d_ell != nullptr && (lb == 4 || lb == 5) &&
+                   c->mode != FW_PROPOSE_CUTEDGE && !(e && e[0] == '1')
+               ? 2
+               : 0;
+  }
+  p.off_w = p.lab_bytes;
+  p.off_gsum = p.off_w + (p.wb ? round16(((int64_t)n * p.wb + 7) / 8) : 0);
   p.off_list = p.off_gsum + round16((int64_t)fw_run_gsum_slots(G) * 2);  // u16 slots
   p.lds_bytes = p.off_list + p.qcap * 4;
   if (G > 64 * 16) {
@@ -583,8 +595,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     }
   }
   // a chain's HBM record also holds its group sums (derived-state cache, FwRunParams)
-  const int lab_stride = p.lab_bytes + (int)round16((int64_t)4 * (use16 ? (G + 1) / 2
-                                                                       : (fw_run_gsum_slots(G) + 1) / 2));
+  const int lab_stride = p.off_gsum + (int)round16((int64_t)4 * (use16 ? (G + 1) / 2
+                                                                      : (fw_run_gsum_slots(G) + 1) / 2));
   std::vector<uint8_t> packed((size_t)n_chains * lab_stride);
   std::vector<int64_t> pops((size_t)n_chains * k);
   {

@@ -811,6 +811,7 @@ struct Ctx {
   FwGraphDev g;
   LDS uint8_t* lab;
   LDS uint16_t* gsum;  // u16 group sums (<= 64 nodes x weight <= 63), gsum_slot layout
+  LDS uint32_t* wts;   // select<.., WB>: 2-bit per-node weights (node x at bits 2x), saturated at 3
   LDS uint32_t* list;  // LDS part of the search list
   GLB uint32_t* spill; // HBM part (this workgroup's slice)
   GLB uint32_t* gscr;  // LB == 3, 5: this workgroup's 4-bit visit marks in HBM (all zero
@@ -1070,7 +1071,7 @@ struct Ctx {
   // -------------------------------------------------------------- select
   // rank r in [0, P) -> node v and in-node index j (canonical (node, ·) order).
   // PER = group sums held per lane (compile-time bound, >= ceil(G/64)).
-  template <int MODE, int PER>
+  template <int MODE, int PER, bool WB = false>
   __device__ __forceinline__ void select(uint32_t r, int G, int& v, uint32_t& j) const {
     static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
     constexpr int SD = gsum_stride_dw(PER);
@@ -1114,7 +1115,15 @@ struct Ctx {
     }
     const int x = gi * 64 + lane;
     uint32_t wx = 0, cd;
-    if constexpr (E16) {
+    if constexpr (E16 && WB) {
+      // the group's weights from LDS; a saturated one (>= 3: four districts around a node,
+      // a few groups in a hundred at C4) from its padded row
+      wx = x < g.n ? (wts[x >> 4] >> ((x & 15) << 1)) & 3u : 0u;
+      if (ballot(wx == 3u)) {
+        const int md = rfl(g.dbound[g.n + gi]);
+        if (wx == 3u) weight_row<MODE>(x, md, wx, cd);
+      }
+    } else if constexpr (E16) {
       // the group's rows are walked up to its largest degree (C4: 9.7 on average, not 14)
 #ifdef FW_VAR_NODB
       const int md = g.maxdeg;
@@ -1274,55 +1283,292 @@ struct Ctx {
     return verdict == 1;
   }
 
+  // race_search_b3's start when a bitboard stage hands its race over: the class codes, the
+  // stage's displaced group-sum words, the head of the visit list (n1 entries of level L - 1,
+  // then the n2 of level L, marked and staged), the processed cells (per-lane partial
+  // counts) and the two classes' representative sources
+  struct B3Run {
+    uint32_t codes, ambig, sv0, sv1, pc, pdeg;
+    int n1, n2, ra, rb;
+    bool ok;
+  };
+
+  // race_search_b3's class codes: the unused labels k..7 first, then borrowed district
+  // labels (ambiguous: bit o), preferring those absent from a sample of 256 cells around v
+  // (a 16 x 16 lattice of step 4): a code met by a frontier is then rarely a real district
+  // cell, so merge tests stay rare.  3-bit code of class o at bits 3o.
+  __device__ void b3_codes(int v, uint32_t a, int m, uint32_t& codes, uint32_t& ambig) const {
+    codes = 0;
+    ambig = 0;
+    int vr, vc;
+    divmod(v, vr, vc);
+    uint32_t seen = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int cell = lane + WAVE * t;  // 0..255
+      const int rr = vr + 4 * (cell >> 4) - 30, cc = vc + 4 * (cell & 15) - 30;
+      if (rr >= 0 && rr < g.gh && cc >= 0 && cc < g.gw) seen |= 1u << L(rr * g.gw + cc);
+    }
+    seen = wave_or32(seen);
+    int o = 0;
+    for (uint32_t c = (uint32_t)k; c < 8u && o < m; ++c, ++o) codes |= c << (3 * o);
+    for (int pass = 0; pass < 2; ++pass)  // absent labels first, then present ones
+      for (uint32_t t = 1; t < 8u && o < m; ++t) {
+        const uint32_t c = (a + t) & 7u;
+        if (c >= (uint32_t)k || ((seen >> c) & 1u) != (uint32_t)pass) continue;
+        codes |= c << (3 * o);
+        ambig |= 1u << o;
+        ++o;
+      }
+  }
+
+  // The two-class race continued on a 128 x 128 window when grid_race_bb2's left its 64 x 64
+  // one (C5's steady state: 19% of the exact searches at base 0.1 after 10^5 steps leave the
+  // 64 x 64 window, 3% the 128 x 128 one; scripts/search_stats.c).  Lane j holds grid rows
+  // vr - 64 + 2j (p = 0) and vr - 63 + 2j (p = 1), dword d of a row the columns vc - 64 + 32d
+  // ...; four dwords per row, eight VGPRs per set.  The race is breadth-first, so the cells
+  // a level meets lie in the previous level Q, the frontier F or the next level: the visited
+  // set is never needed, only Q (the sets are A, Fa, Fb, Q).  The levels, merges, stopping
+  // rules and counters are grid_race_bb2's.  When a frontier about to be processed holds a
+  // window-edge cell whose outward neighbour is on the grid it returns -1, having written
+  // the list search's start (B3Run): level L (the frontier) and the cells of level L - 1
+  // next to it take their class's code and head the visit list.  The rest of level L - 1
+  // is never met again: its neighbours lie at levels L - 2 .. L, and level L is F.
+  template <int ND>
+  __device__ int race_bb4(int v, int vr, int vc, uint32_t a, int m, const BBSeed& s2,
+                          uint64_t& bfs_nodes, uint64_t& bfs_deg, B3Run& rs) {
+    const int W = g.gw, H = g.gh;
+    constexpr int WC = 32 * ND;  // window columns
+    const int R0 = vr - 64, C0 = vc - WC / 2;
+    const int re = R0 + 2 * lane;
+    // a-labelled cells of dword d of row p (v excluded)
+    auto district = [&](int p, int d) -> uint32_t {
+      const int r = re + p, cb = C0 + 32 * d;
+      if (r < 0 || r >= H) return 0u;
+      uint32_t mk = cb <= -32 ? 0u : (cb < 0 ? ~0u << (-cb) : ~0u);
+      const int hi = W - cb;
+      if (hi < 32) mk &= hi <= 0 ? 0u : (1u << hi) - 1u;
+      uint32_t x = eq_bits32<LB>(lab, g.n, r * W + cb, a) & mk;
+      if (lane == 32 && p == 0 && d == (WC / 2) / 32) x &= ~(1u << ((WC / 2) % 32));  // v
+      return x;
+    };
+    // bb2's 64 x 64 state: its lane i (row vr - 32 + i) is row 32 + i here, i.e. lane
+    // 16 + i / 2, p = i & 1; its 64 columns start at window column WC / 2 - 32
+    const bool tin = lane >= 16 && lane < 48;
+    const int se = tin ? 2 * (lane - 16) : 0;
+    auto xfer = [&](uint32_t x, int p) -> uint32_t {
+      const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((se + p) << 2, (int)x);
+      return tin ? y : 0u;
+    };
+    // a 64-column row (x1:x0) placed at window column WC / 2 - 32, as dword d
+    auto place = [](uint32_t x0, uint32_t x1, int d) -> uint32_t {
+      if constexpr (ND == 4) {
+        return d == 1 ? x0 : d == 2 ? x1 : 0u;
+      } else {
+        static_assert(ND == 3, "race_bb4: 96- or 128-column windows");
+        return d == 0 ? x0 << 16 : d == 1 ? (x0 >> 16) | (x1 << 16) : x1 >> 16;
+      }
+    };
+    // U: the district's cells not yet reached (bb2's last two levels removed; its older
+    // levels stay in U but are never met again), F: the frontier of each class
+    uint32_t U[2][ND], Fa[2][ND], Fb[2][ND];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const uint32_t fa0 = xfer(s2.fa0, p), fa1 = xfer(s2.fa1, p);
+      const uint32_t fb0 = xfer(s2.fb0, p), fb1 = xfer(s2.fb1, p);
+      const uint32_t q0 = xfer(s2.qa0 | s2.qb0, p), q1 = xfer(s2.qa1 | s2.qb1, p);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        Fa[p][d] = place(fa0, fa1, d);
+        Fb[p][d] = place(fb0, fb1, d);
+        U[p][d] = district(p, d) & ~(place(q0, q1, d) | Fa[p][d] | Fb[p][d]);
+      }
+    }
+    uint32_t pc = s2.pc, pdeg = s2.pdeg;  // processed cells (bb2's, then this window's)
+    // on-grid degree of a cell: per row, minus one in grid columns 0 and W - 1
+    const uint32_t fdeg0 = (uint32_t)((re > 0) + (re < H - 1) + 2);
+    const uint32_t fdeg1 = (uint32_t)((re + 1 > 0) + (re + 1 < H - 1) + 2);
+    const int w0 = -C0, w1 = W - 1 - C0;  // window positions of grid columns 0 and W - 1
+    auto wbit = [](const uint32_t (&f)[ND], int pos) -> uint32_t {
+      uint32_t dd = f[0];
+#pragma unroll
+      for (int d = 1; d < ND; ++d)
+        if (pos >= 32 * d) dd = f[d];
+      return (dd >> (pos & 31)) & 1u;
+    };
+    // window-edge cells with an on-grid neighbour outside the window
+    const bool e_top = lane == 0 && R0 > 0, e_bot = lane == 63 && R0 + 127 < H - 1;
+    const bool e_left = C0 > 0, e_right = C0 + WC - 1 < W - 1;
+    for (;;) {
+      bool edge = false;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint32_t any = 0u;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) any |= Fa[p][d] | Fb[p][d];
+        edge |= (e_left && ((Fa[p][0] | Fb[p][0]) & 1u)) || (e_right && ((Fa[p][ND - 1] | Fb[p][ND - 1]) >> 31));
+        if (p == 0 ? e_top : e_bot) edge |= any != 0u;
+      }
+      if (ballot(edge)) break;
+      // this level's frontier is processed: count it
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint32_t f[ND];
+        uint32_t c = 0;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          f[d] = Fa[p][d] | Fb[p][d];
+          c += (uint32_t)__popc(f[d]);
+        }
+        pc += c;
+        uint32_t dg = c * (p == 0 ? fdeg0 : fdeg1);
+        if (w0 >= 0 && w0 < WC) dg -= wbit(f, w0);
+        if (w1 >= 0 && w1 < WC) dg -= wbit(f, w1);
+        pdeg += dg;
+      }
+      // dilations, the new cells and the merge test, one column of dwords at a time (both
+      // rows), updating the sets in place: the old values a later dword needs (its left
+      // neighbour's carry) are held in pa / pb, and the other lanes' rows are read by DPP
+      // before this dword of theirs is updated (one instruction stream).  bb2's merge test
+      // D_a & (F_b | (D_b & new)) is (dil F_a & F_b) | (dil F_a & dil F_b & U) here
+      bool met = false;
+      bool any_a = false, any_b = false;
+      uint32_t pa0 = 0u, pa1 = 0u, pb0 = 0u, pb1 = 0u;  // old F of dword d - 1, rows 0 / 1
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const uint32_t a0 = Fa[0][d], a1 = Fa[1][d], b0 = Fb[0][d], b1 = Fb[1][d];
+        const uint32_t na0 = d < ND - 1 ? Fa[0][d + 1] : 0u, na1 = d < ND - 1 ? Fa[1][d + 1] : 0u;
+        const uint32_t nb0 = d < ND - 1 ? Fb[0][d + 1] : 0u, nb1 = d < ND - 1 ? Fb[1][d + 1] : 0u;
+        const uint32_t ra0 = a0 | (a0 << 1) | (a0 >> 1) | (pa0 >> 31) | (na0 << 31) | from_prev_lane(a1) | a1;
+        const uint32_t ra1 = a1 | (a1 << 1) | (a1 >> 1) | (pa1 >> 31) | (na1 << 31) | a0 | from_next_lane(a0);
+        const uint32_t rb0 = b0 | (b0 << 1) | (b0 >> 1) | (pb0 >> 31) | (nb0 << 31) | from_prev_lane(b1) | b1;
+        const uint32_t rb1 = b1 | (b1 << 1) | (b1 >> 1) | (pb1 >> 31) | (nb1 << 31) | b0 | from_next_lane(b0);
+        const uint32_t da0 = ra0 & U[0][d], da1 = ra1 & U[1][d];
+        const uint32_t db0 = rb0 & U[0][d], db1 = rb1 & U[1][d];
+        met |= ((ra0 & b0) | (ra1 & b1) | (da0 & db0) | (da1 & db1)) != 0u;
+        Fa[0][d] = da0;
+        Fa[1][d] = da1;
+        Fb[0][d] = db0;
+        Fb[1][d] = db1;
+        U[0][d] &= ~(da0 | db0);
+        U[1][d] &= ~(da1 | db1);
+        any_a |= (da0 | da1) != 0u;
+        any_b |= (db0 | db1) != 0u;
+        pa0 = a0;
+        pa1 = a1;
+        pb0 = b0;
+        pb1 = b1;
+      }
+      if (ballot(met) || !ballot(any_a) || !ballot(any_b)) {
+        // the two classes met: connected; or a class reached no new cell: closed
+        bfs_nodes += wave_sum(pc);
+        bfs_deg += wave_sum(pdeg);
+        return ballot(met) ? 1 : 0;
+      }
+    }
+    // left the window: hand the race to the list search
+#ifdef FW_EXP1
+    return -1;
+#endif
+    b3_codes(v, a, m, rs.codes, rs.ambig);
+    LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
+    rs.sv0 = lane < scap ? stage[lane] : 0u;
+    rs.sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
+    lds_order();
+    // level L - 1 cells next to each class's frontier: reached district cells (not in U, not
+    // in F) adjacent to it (a level L - 1 cell adjacent to both classes would have merged
+    // them); U is turned into those reached cells
+    uint32_t c1 = 0, c2 = 0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        U[p][d] = district(p, d) & ~(U[p][d] | Fa[p][d] | Fb[p][d]);
+        c2 += (uint32_t)(__popc(Fa[p][d]) + __popc(Fb[p][d]));
+      }
+    auto adj = [&](const uint32_t (&X)[2][ND], int p, int d) -> uint32_t {
+      const uint32_t x = X[p][d], pv = d > 0 ? X[p][d - 1] : 0u, nx = d < ND - 1 ? X[p][d + 1] : 0u;
+      uint32_t h = x | (x << 1) | (x >> 1) | (pv >> 31) | (nx << 31);
+      h |= p == 0 ? (from_prev_lane(X[1][d]) | X[1][d]) : (X[0][d] | from_next_lane(X[0][d]));
+      return h;
+    };
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+        c1 += (uint32_t)(__popc(U[p][d] & adj(Fa, p, d)) + __popc(U[p][d] & adj(Fb, p, d)));
+    const uint32_t i1 = scan_incl(c1), i2 = scan_incl(c2);
+    const int n1 = (int)rdl(i1, 63), n2 = (int)rdl(i2, 63);
+    const uint32_t ca = (rs.codes >> (3 * s2.ra)) & 7u, cb = (rs.codes >> (3 * s2.rb)) & 7u;
+    // one class's cells of one dword of one of this lane's rows, from list index idx on
+    auto emit = [&](uint32_t bits, int row, int col, uint32_t o, uint32_t code, int& idx,
+                    bool staged) {
+      while (bits) {
+        const int t = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const int x = row * W + col + t;
+        const uint32_t e = (uint32_t)x | (o << 16);
+        spill[idx] = e;
+        if (staged && idx - n1 < scap) stage[idx - n1] = e;
+        P::axor(lab, x, a ^ code);
+        ++idx;
+      }
+    };
+    int idx = (int)(i1 - c1);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        emit(U[p][d] & adj(Fa, p, d), re + p, C0 + 32 * d, (uint32_t)s2.ra, ca, idx, false);
+        emit(U[p][d] & adj(Fb, p, d), re + p, C0 + 32 * d, (uint32_t)s2.rb, cb, idx, false);
+      }
+    idx = n1 + (int)(i2 - c2);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        emit(Fa[p][d], re + p, C0 + 32 * d, (uint32_t)s2.ra, ca, idx, true);
+        emit(Fb[p][d], re + p, C0 + 32 * d, (uint32_t)s2.rb, cb, idx, true);
+      }
+    rs.pc = pc;
+    rs.pdeg = pdeg;
+    rs.n1 = n1;
+    rs.n2 = n2;
+    rs.ra = s2.ra;
+    rs.rb = s2.rb;
+    rs.ok = true;
+    return -1;
+  }
+
   // The race search of 3-bit-label grids (C5's 200x200 chains) with its visit marks in the
   // labels themselves: the levels, pushes, merges and counters of race_search_gscr and of
   // the oracle's contiguous_after, with LDS round trips where an HBM-marked search pays
   // memory-side atomics (global atomics execute past the XCD's L2).  A claimed node's label
-  // a becomes its class's code: the unused labels k..7 first, then district labels absent
-  // from a 256-cell sample around v.  A borrowed code is ambiguous (a cell of that district,
-  // or a visited one): when a frontier node of one class meets the code of another, unmerged
-  // class (the merge test), the node is looked up among the entries of the current level
-  // and of the next level so far.  That is complete: the race is breadth-first, so a visited
-  // neighbour of a level-L node lies at level L - 1, L or L + 1, and one of another class at
-  // level L - 1 would already have merged the two classes.  Within a level the four
-  // neighbour directions run one after another, so a node claimed in an earlier direction
-  // reads as claimed (LDS ops of one wave execute in program order) and no node is pushed
-  // twice: on a grid two frontier nodes reach the same node in one direction only if they
-  // are the same node.  A list entry carries its class (node | class << 16).  The next level
-  // is staged in LDS over the chain's group sums (not read while the search runs; up to scap
-  // entries, the displaced words held in two VGPRs); every entry also goes to the HBM visit
-  // list (coalesced 4-byte stores), from which a larger level is read and the labels are
-  // restored at the end.  With a seed (grid_race_bb2's two-class race left its 64 x 64
-  // window), the race continues from the bitboard's last two levels instead of from the
-  // sources.
+  // a becomes its class's code (b3_codes).  A borrowed code is ambiguous (a cell of that
+  // district, or a visited one): when a frontier node of one class meets the code of
+  // another, unmerged class (the merge test), the node is looked up among the entries of
+  // the current level and of the next level so far.  That is complete: the race is
+  // breadth-first, so a visited neighbour of a level-L node lies at level L - 1, L or L + 1,
+  // and one of another class at level L - 1 would already have merged the two classes.
+  // Within a level the four neighbour directions run one after another, so a node claimed
+  // in an earlier direction reads as claimed (LDS ops of one wave execute in program order)
+  // and no node is pushed twice: on a grid two frontier nodes reach the same node in one
+  // direction only if they are the same node.  A list entry carries its class (node |
+  // class << 16).  The next level is staged in LDS over the chain's group sums (not read
+  // while the search runs; up to scap entries, the displaced words held in two VGPRs);
+  // every entry also goes to the HBM visit list (coalesced 4-byte stores), from which a
+  // larger level is read and the labels are restored at the end.  With rs.ok (race_bb4's
+  // two-class race left its 128 x 128 window) the race continues from the head of the
+  // list race_bb4 wrote instead of from the sources.
   __device__ bool race_search_b3(int v, uint32_t a, int m, int src, uint64_t cls, int scap,
-                                 const BBSeed& sd, uint64_t& bfs_nodes, uint64_t& bfs_deg) {
+                                 const B3Run& rs, uint64_t& bfs_nodes, uint64_t& bfs_deg) {
     LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
-    // class codes: unused labels first, then borrowed ones, preferring district labels
-    // absent from a sample of 256 cells around v (a 16 x 16 lattice of step 4): a code
-    // met by a frontier is then rarely a real district cell, so merge tests stay rare
-    uint32_t codes = 0, ambig = 0;  // 3-bit code of class o at bits 3o; ambiguous: bit o
-    {
-      int vr, vc;
-      divmod(v, vr, vc);
-      uint32_t seen = 0;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int cell = lane + WAVE * t;  // 0..255
-        const int rr = vr + 4 * (cell >> 4) - 30, cc = vc + 4 * (cell & 15) - 30;
-        if (rr >= 0 && rr < g.gh && cc >= 0 && cc < g.gw) seen |= 1u << L(rr * g.gw + cc);
-      }
-      seen = wave_or32(seen);
-      int o = 0;
-      for (uint32_t c = (uint32_t)k; c < 8u && o < m; ++c, ++o) codes |= c << (3 * o);
-      for (int pass = 0; pass < 2; ++pass)  // absent labels first, then present ones
-        for (uint32_t t = 1; t < 8u && o < m; ++t) {
-          const uint32_t c = (a + t) & 7u;
-          if (c >= (uint32_t)k || ((seen >> c) & 1u) != (uint32_t)pass) continue;
-          codes |= c << (3 * o);
-          ambig |= 1u << o;
-          ++o;
-        }
+    uint32_t codes, ambig;
+    if (rs.ok) {
+      codes = rs.codes;
+      ambig = rs.ambig;
+    } else {
+      b3_codes(v, a, m, codes, ambig);
     }
     // code -> class + 1 (0: not a class code), 8 entries of 3 bits
     uint32_t cls_of = 0;
@@ -1341,8 +1587,14 @@ struct Ctx {
       for (int i = 0; i < m; ++i) nc += (__ffs((M >> (4 * i)) & 15u) - 1) == i;
       return nc;
     };
-    const uint32_t sv0 = lane < scap ? stage[lane] : 0u;
-    const uint32_t sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
+    uint32_t sv0, sv1;
+    if (rs.ok) {
+      sv0 = rs.sv0;
+      sv1 = rs.sv1;
+    } else {
+      sv0 = lane < scap ? stage[lane] : 0u;
+      sv1 = lane + WAVE < scap ? stage[lane + WAVE] : 0u;
+    }
     lds_order();
     int lb = 0, le = m;
     uint32_t my_deg = 0;
@@ -1379,51 +1631,16 @@ struct Ctx {
       }
       return hit;
     };
-    if (sd.ok) {
-      // continue grid_race_bb2's race where it left its window: its last two levels take
-      // their class's code and form the head of the visit list (the previous level, then
-      // the current one); the cells processed before are never met again and are counted
-      // as the bitboard counts them
+    if (rs.ok) {
 #ifdef FW_STAMPS
       n_seed += 1;
 #endif
-      int vr, vc;
-      divmod(v, vr, vc);
-      const int r = vr - 32 + lane, c0 = vc - 32;
-      const uint32_t c1 = (uint32_t)(__popc(sd.qa0) + __popc(sd.qa1) + __popc(sd.qb0) + __popc(sd.qb1));
-      const uint32_t c2 = (uint32_t)(__popc(sd.fa0) + __popc(sd.fa1) + __popc(sd.fb0) + __popc(sd.fb1));
-      const uint32_t i1 = scan_incl(c1), i2 = scan_incl(c2);
-      const int n1 = (int)rdl(i1, 63), n2 = (int)rdl(i2, 63);
-      const uint32_t ca = (codes >> (3 * sd.ra)) & 7u, cb = (codes >> (3 * sd.rb)) & 7u;
-      // one class's cells of one dword of this lane's row, from list index idx on
-      auto emit = [&](uint32_t bits, int col, uint32_t o, uint32_t code, int& idx, bool staged) {
-        while (bits) {
-          const int t = __ffs(bits) - 1;
-          bits &= bits - 1;
-          const int x = r * g.gw + col + t;
-          const uint32_t e = (uint32_t)x | (o << 16);
-          spill[idx] = e;
-          if (staged && idx - n1 < scap) stage[idx - n1] = e;
-          P::axor(lab, x, a ^ code);
-          ++idx;
-        }
-      };
-      int idx = (int)(i1 - c1);
-      emit(sd.qa0, c0, (uint32_t)sd.ra, ca, idx, false);
-      emit(sd.qa1, c0 + 32, (uint32_t)sd.ra, ca, idx, false);
-      emit(sd.qb0, c0, (uint32_t)sd.rb, cb, idx, false);
-      emit(sd.qb1, c0 + 32, (uint32_t)sd.rb, cb, idx, false);
-      idx = n1 + (int)(i2 - c2);
-      emit(sd.fa0, c0, (uint32_t)sd.ra, ca, idx, true);
-      emit(sd.fa1, c0 + 32, (uint32_t)sd.ra, ca, idx, true);
-      emit(sd.fb0, c0, (uint32_t)sd.rb, cb, idx, true);
-      emit(sd.fb1, c0 + 32, (uint32_t)sd.rb, cb, idx, true);
-      // the bitboard's counters over the processed cells (grid_race_bb2)
-      my_deg += sd.pdeg;
-      nodes += (uint64_t)wave_sum(sd.pc);
-      lb = n1;
-      le = n1 + n2;
-      if (n2 > scap) __threadfence_block();  // the level is read from the HBM list
+      // the bitboards' counters over their processed cells
+      my_deg += rs.pdeg;
+      nodes += (uint64_t)wave_sum(rs.pc);
+      lb = rs.n1;
+      le = rs.n1 + rs.n2;
+      if (rs.n2 > scap) __threadfence_block();  // the level is read from the HBM list
     } else if (lane < m) {
       const uint32_t e = (uint32_t)src | ((uint32_t)lane << 16);
       P::axor(lab, src, a ^ ((codes >> (3 * lane)) & 7u));
@@ -1432,11 +1649,11 @@ struct Ctx {
     }
     lds_order();
     int verdict = -1;
-    if (sd.ok) {
+    if (rs.ok) {
       // the seeded race has two classes: one code test per neighbour, a merge ends it
-      const uint32_t oa = (uint32_t)sd.ra;
-      const uint32_t ca = (codes >> (3 * sd.ra)) & 7u, cb = (codes >> (3 * sd.rb)) & 7u;
-      const bool ma = (ambig >> sd.ra) & 1u, mb = (ambig >> sd.rb) & 1u;
+      const uint32_t oa = (uint32_t)rs.ra;
+      const uint32_t ca = (codes >> (3 * rs.ra)) & 7u, cb = (codes >> (3 * rs.rb)) & 7u;
+      const bool ma = (ambig >> rs.ra) & 1u, mb = (ambig >> rs.rb) & 1u;
       for (;;) {
         const int cnt = le - lb;
         const bool staged = cnt <= scap;
@@ -1787,8 +2004,8 @@ struct Ctx {
     if (m == 1) return true;
     CTX_T0
     uint64_t cls = lane < m ? (1ull << lane) : 0ull;
-    BBSeed sd;
-    sd.ok = false;
+    B3Run rs;
+    rs.ok = false;
     // source index (rank in am) of the source held by lane ln
     auto sx = [&](int ln) { return __popcll(am & ((1ull << ln) - 1ull)); };
     auto merge = [&](int s1, int s2) {
@@ -1849,11 +2066,16 @@ struct Ctx {
         const uint32_t lk = (uint32_t)(lNE | (lES << 1) | (lSW << 2) | (lWN << 3));
         int wv;
         if constexpr (LB == 3) {
+          BBSeed s2;
           wv = grid_race_bb2<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk, bfs_nodes,
-                                 bfs_deg, sd);
-          if (sd.ok) {  // the classes' source indices (CSR order of v's neighbours)
-            sd.ra = sx(sd.ra + 1);
-            sd.rb = sx(sd.rb + 1);
+                                 bfs_deg, s2);
+          if (s2.ok) {  // the classes' source indices (CSR order of v's neighbours)
+            s2.ra = sx(s2.ra + 1);
+            s2.rb = sx(s2.rb + 1);
+#ifndef FW_BB4_ND
+#define FW_BB4_ND 4
+#endif
+            wv = race_bb4<FW_BB4_ND>(v, vr, vc, a, m, s2, bfs_nodes, bfs_deg, rs);
           }
         } else {
           wv = grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk, bfs_nodes,
@@ -1889,7 +2111,7 @@ struct Ctx {
     }
     bool verdict;
     if constexpr (LB == 3 && GRID)
-      verdict = race_search_b3(v, a, m, src, cls, scap, sd, bfs_nodes, bfs_deg);
+      verdict = race_search_b3(v, a, m, src, cls, scap, rs, bfs_nodes, bfs_deg);
     else if constexpr (LB == 3 || LB == 5)
       verdict = race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else

@@ -66,6 +66,9 @@ struct FwRunParams {
   // LDS layout (bytes from the dynamic shared base)
   int32_t lab_bytes;           // packed label bytes (multiple of 16)
   int32_t off_gsum, off_list, lds_bytes;
+  // chain kernel on padded rows, pairs proposals: 2-bit per-node proposal weights at off_w
+  // (between the labels and the group sums), saturated at 3 (wb = 2; 0: none)
+  int32_t off_w, wb;
   int32_t off_ssum;            // grid kernel, large grids: supergroup sums in the slot
   int32_t lb;                  // label bits per node (2, 4 or 8)
   int32_t use16;               // 1: launch the four-chains-per-wave grid kernel

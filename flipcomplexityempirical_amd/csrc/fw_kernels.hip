@@ -60,7 +60,8 @@ namespace {
 // WPE: waves per SIMD the register budget targets (5 only where LDS admits 20 chains per CU)
 // FULL = false: the lean instantiation for the common configuration (cut_accept, no
 // spatial maps, ring observable, bound schedule or trace), as in fw_grid16_kernel
-template <int LB, bool GRID, int MODE, int PER, bool E16, int WPE = 4, bool FULL = true>
+// WB: 2-bit per-node weights in LDS (padded rows, pairs proposals; FwRunParams::wb)
+template <int LB, bool GRID, int MODE, int PER, bool E16, int WPE = 4, bool FULL = true, bool WB = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void fw_run_kernel(FwRunParams p) {
   extern __shared__ __align__(16) uint8_t smem[];
   Ctx<LB, GRID, E16> C;
@@ -68,6 +69,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   LDS uint8_t* const sm = (LDS uint8_t*)smem;
   C.lab = sm;
   C.gsum = reinterpret_cast<LDS uint16_t*>(sm + p.off_gsum);
+  C.wts = reinterpret_cast<LDS uint32_t*>(sm + p.off_w);
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
   C.gscr = LB == 3 || LB == 5 ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
@@ -159,10 +161,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       npairs = rfl(stp->npairs);
     } else {
       uint32_t cut2 = 0, bn = 0, np = 0;
+      if constexpr (WB) {
+        for (int i = lane; i < (n + 15) / 16; i += WAVE) C.wts[i] = 0u;
+        lds_order();
+      }
       for (int t = 0; t < G; ++t) {
         const int x = t * 64 + lane;
         uint32_t w = 0, cd = 0;
         if (x < n) C.template weight_now<MODE>(x, w, cd);
+        if (WB && x < n) __atomic_fetch_or(C.wts + (x >> 4), min(w, 3u) << ((x & 15) << 1), __ATOMIC_RELAXED);
         const uint32_t gsum_t = wave_sum(w);
         if (lane == 0) C.gsum[gsum_slot<PER>(t)] = (uint16_t)gsum_t;  // <= 64 x 63
         cut2 += cd;
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const uint32_t r = scale64(x.x0, x.x1, (uint32_t)npairs);
         uint32_t j = 0;
         CSTAMP(0);  // draw
-        C.template select<MODE, PER>(r, G, v, j);
+        C.template select<MODE, PER, WB>(r, G, v, j);
         CSTAMP(1);  // select
         v = rfl(v);
         if (v < 0) {  // internal inconsistency: stop this chain, flag it
@@ -400,6 +407,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           // only that half (both halves stay in [0, 65535])
           const int sl = gsum_slot<PER>(h.x >> 6);
           lds_add(reinterpret_cast<LDS uint32_t*>(C.gsum) + (sl >> 1), (wn - wo) << (16 * (sl & 1)));
+          if constexpr (WB) {
+            const uint32_t so = min(wo, 3u), sn = min(wn, 3u);
+            if (so != sn)
+              __atomic_fetch_xor(C.wts + (h.x >> 4), (so ^ sn) << ((h.x & 15) << 1), __ATOMIC_RELAXED);
+          }
         }
         lds_order();
         npairs += (int32_t)wave_sum(mine ? wn - wo : 0u);
@@ -631,31 +643,37 @@ int fw_run_gsum_slots(int G) {
 
 namespace {
 
-template <int LB, bool GRID, int MODE, bool E16, int WPE = 4, bool FULL = true>
+template <int LB, bool GRID, int MODE, bool E16, int WPE = 4, bool FULL = true, bool WB = false>
 void* pick_per(int G) {
   switch (fw_run_per(G)) {
-    case 2: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE, FULL>);
-    case 4: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE, FULL>);
-    case 8: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE, FULL>);
-    case 10: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 10, E16, WPE, FULL>);
-    default: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE, FULL>);
+    case 2: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 2, E16, WPE, FULL, WB>);
+    case 4: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 4, E16, WPE, FULL, WB>);
+    case 8: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 8, E16, WPE, FULL, WB>);
+    case 10: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 10, E16, WPE, FULL, WB>);
+    default: return reinterpret_cast<void*>(&fw_run_kernel<LB, GRID, MODE, 16, E16, WPE, FULL, WB>);
   }
 }
 
+// padded rows, pairs proposals (4- or 5-bit labels): with or without the LDS weights
+template <int LB, int WPE, bool FULL>
+void* pick_e16_pairs(int G, bool wb) {
+  return wb ? pick_per<LB, false, 1, true, WPE, FULL, true>(G) : pick_per<LB, false, 1, true, WPE, FULL>(G);
+}
+
 template <bool FULL>
-void* pick_run_t(int lb, bool grid, bool e16, int mode, int G, bool wpe5) {
+void* pick_run_t(int lb, bool grid, bool e16, int mode, int G, bool wpe5, bool wb) {
   const bool cut = mode == FW_PROPOSE_CUTEDGE;
   if (lb == 4) {
     // small general graphs (4-bit labels, padded rows): a 5-waves-per-SIMD register budget
     if (!grid && e16 && wpe5)
-      return cut ? pick_per<4, false, 2, true, 5, FULL>(G) : pick_per<4, false, 1, true, 5, FULL>(G);
+      return cut ? pick_per<4, false, 2, true, 5, FULL>(G) : pick_e16_pairs<4, 5, FULL>(G, wb);
     if (grid) return cut ? pick_per<4, true, 2, false, 4, FULL>(G) : pick_per<4, true, 1, false, 4, FULL>(G);
-    if (e16) return cut ? pick_per<4, false, 2, true, 4, FULL>(G) : pick_per<4, false, 1, true, 4, FULL>(G);
+    if (e16) return cut ? pick_per<4, false, 2, true, 4, FULL>(G) : pick_e16_pairs<4, 4, FULL>(G, wb);
     return cut ? pick_per<4, false, 2, false, 4, FULL>(G) : pick_per<4, false, 1, false, 4, FULL>(G);
   }
   if (lb == 5)  // general graphs with padded rows, 16 <= k <= 31 (fw_chains_create)
-    return !grid && e16 ? (wpe5 ? (cut ? pick_per<5, false, 2, true, 5, FULL>(G) : pick_per<5, false, 1, true, 5, FULL>(G))
-                                : (cut ? pick_per<5, false, 2, true, 4, FULL>(G) : pick_per<5, false, 1, true, 4, FULL>(G)))
+    return !grid && e16 ? (wpe5 ? (cut ? pick_per<5, false, 2, true, 5, FULL>(G) : pick_e16_pairs<5, 5, FULL>(G, wb))
+                                : (cut ? pick_per<5, false, 2, true, 4, FULL>(G) : pick_e16_pairs<5, 4, FULL>(G, wb)))
                         : nullptr;
   if (lb == 3)  // grids, k <= 8 (the large-grid LDS plan: fw_chains_create)
     return grid ? (cut ? pick_per<3, true, 2, false, 3, FULL>(G) : pick_per<3, true, 1, false, 3, FULL>(G))
@@ -668,8 +686,10 @@ void* pick_run_t(int lb, bool grid, bool e16, int mode, int G, bool wpe5) {
 // grids: implicit neighbours; general graphs: the padded 16-wide table when it exists.
 // The LDS plan and residency are sized on the FULL instantiation (the optional features
 // can be switched on after fw_chains_create); launches take the lean one when they are off.
-void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false, bool full = true) {
-  return full ? pick_run_t<true>(lb, grid, e16, mode, G, wpe5) : pick_run_t<false>(lb, grid, e16, mode, G, wpe5);
+void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false, bool full = true,
+               bool wb = false) {
+  return full ? pick_run_t<true>(lb, grid, e16, mode, G, wpe5, wb)
+              : pick_run_t<false>(lb, grid, e16, mode, G, wpe5, wb);
 }
 
 }  // namespace
@@ -677,7 +697,7 @@ void* pick_run(int lb, bool grid, bool e16, int mode, int G, bool wpe5 = false, 
 // Occupancy-sized persistent grid for the one-chain-per-wave kernel.
 int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   if (p.G > 64 * 16) return -2;
-  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G);
+  void* fn = pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, false, true, p.wb != 0);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   if (e != hipSuccess) return -1;
   int per_cu = 0;
@@ -717,7 +737,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   // register budget, the 5-wave instantiation (Frankengraph: 16 -> 20 chains per CU, +4%)
   p.wpe5 = 0;
   if ((lb == 4 || lb == 5) && p.g.gw == 0 && p.g.ell != nullptr) {
-    void* fn5 = pick_run(lb, false, true, p.mode, p.G, true);
+    void* fn5 = pick_run(lb, false, true, p.mode, p.G, true, true, p.wb != 0);
     if (hipFuncSetAttribute(fn5, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
         hipSuccess)
       return -1;
@@ -745,7 +765,7 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
 void* fw_run_fn(const FwRunParams& p, int lb) {
   const bool full = p.m_acc != nullptr || p.accept != FW_ACCEPT_CUT || p.sched != nullptr ||
                     p.ring_n > 0 || p.trace != nullptr || p.wsamp != nullptr;
-  return pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0, full);
+  return pick_run(lb, p.g.gw > 0, p.g.ell != nullptr, p.mode, p.G, p.wpe5 != 0, full, p.wb != 0);
 }
 
 int fw_launch_run(const FwRunParams& p, int lb, int grid, void* stream) {
