@@ -225,8 +225,8 @@ def pmc_key(config, order, chains, inner, steady):
     on this GPU, steps per launch, and whether the chains were resumed at the steady state."""
     from flipcomplexityempirical_amd.workloads import C4_ORDER
     name = config
-    if config == "c4" and (order or C4_ORDER) != "random":
-        name += "h"
+    if config == "c4" and (order or C4_ORDER) != "hilbert":
+        name += "r"
     return f"{name}_{chains}_{inner}" + ("_steady" if steady else "")
 
 

@@ -79,7 +79,7 @@ class Workload:
                 f"{', ...' if len(idx) > 8 else ''})")
 
 
-C4_ORDER = "random"  # node numbering of the C4 Delaunay graph (graph.delaunay_graph)
+C4_ORDER = "hilbert"  # node numbering of the C4 Delaunay graph (graph.delaunay_graph)
 
 
 def workload(name: str, grid: Optional[int] = None, k: Optional[int] = None,

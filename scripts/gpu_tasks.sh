@@ -67,16 +67,17 @@ run_task() {
       local lib=${t#prof_c5:}
       FLIPWALK_LIB=$PWD/ab/lib_$lib.so prof c5steady_$lib "--config c5 --shard 0/8 --resume $CK5 --check-chains 0" "--steps 5 --warmup 0 --inner 1000 --no-cpu-baseline --config c5 --shard 0/8 --resume $CK5 --check-chains 0" ;;
     prof_c4) prof c4 "--config c4" ;;
-    prof_c4h) prof c4h "--config c4 --order hilbert" ;;
+    prof_c4r) prof c4r "--config c4 --order random" ;;
+    prof_frank) prof frank "--config frank" ;;
     prof_c3) prof c3 "" ;;
     prof_c2) prof c2 "--config c2" ;;
     prof_c3s8) prof c3s8 "--config c3 --shard 0/8" ;;
     stamps_c5)
       timeout -k 10 300 python -u scripts/stamps.py c5 8192 1 $CK5 > $O/stamps_c5_100k.txt 2>&1 || { tail -5 $O/stamps_c5_100k.txt; return 1; }
       grep -v amdgpu.ids $O/stamps_c5_100k.txt ;;
-    stamps_c4h)
-      timeout -k 10 300 python -u scripts/stamps.py c4h 16384 2 > $O/stamps_c4h.txt 2>&1 || { tail -5 $O/stamps_c4h.txt; return 1; }
-      grep -v amdgpu.ids $O/stamps_c4h.txt ;;
+    stamps_c4r)
+      timeout -k 10 300 python -u scripts/stamps.py c4r 16384 2 > $O/stamps_c4r.txt 2>&1 || { tail -5 $O/stamps_c4r.txt; return 1; }
+      grep -v amdgpu.ids $O/stamps_c4r.txt ;;
     stamps_c4)
       timeout -k 10 300 python -u scripts/stamps.py c4 16384 2 > $O/stamps_c4.txt 2>&1 || { tail -5 $O/stamps_c4.txt; return 1; }
       grep -v amdgpu.ids $O/stamps_c4.txt ;;

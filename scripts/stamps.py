@@ -18,7 +18,7 @@ L.fw_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 # optional checkpoint to resume from first)
 from flipcomplexityempirical_amd.workloads import workload  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
-w = workload("c4", order="hilbert") if cfg == "c4h" else workload(cfg)
+w = workload("c4", order="random") if cfg == "c4r" else workload(cfg)
 nch = int(sys.argv[2]) if len(sys.argv) > 2 else w.chains
 g = w.graph
 dg = DeviceGraph(g)
