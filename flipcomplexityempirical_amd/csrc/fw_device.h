@@ -978,6 +978,23 @@ struct Ctx {
     }
   }
 
+  // E16: v's neighbours (lanes 1..dv) and their labels, from v's padded row only
+  __device__ __forceinline__ Hood gather_ids(int v, int& dv) const {
+    Hood h;
+    h.x = -1;
+    h.lx = NOLAB;
+    h.bits = 0;
+    h.cnt = 0;
+    h.has_v = false;
+    h.deg = 0;
+    const int xn = (lane >= 1 && lane <= 16) ? g.ell[(size_t)v * 16 + lane - 1] : -1;
+    dv = __popcll(ballot(xn >= 0));
+    if (lane > dv) return h;
+    h.x = lane == 0 ? v : xn;
+    h.lx = L(h.x);
+    return h;
+  }
+
   // One LDS round trip: every lane with a role reads its node and (lanes 0..dv) the
   // node's neighbours.
   __device__ __forceinline__ Hood gather(int v, int& dv) const {

@@ -241,6 +241,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     int bpos = WAVE;
 
     const bool unit_pop = p.g.pop == nullptr;
+  // padded rows without the optional features: the neighbours' rows only on accept
+  constexpr bool LAZY = E16 && !GRID && !FULL;
     // wave priority 3 - (level mod 4), the level counting 32nds of the unit's steps: the
     // SIMD's VALU goes to the wave one level behind instead of the oldest (see
     // fw_grid16_kernel), so the waves of the last residency round finish together
@@ -304,7 +306,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         // populations in HBM / L2) overlaps the LDS round trip instead of following it
         pv = unit_pop ? 1 : p.g.pop[v];
         // ---- v's neighbourhood (one LDS round trip)
-        h = C.gather(v, dv);
+        // padded rows, lean kernel: v's row and its neighbours' labels only; the neighbours'
+        // own rows (their label sets, for the weights of v's neighbourhood) are read when a
+        // flip is accepted (C4: 29% of attempts)
+        if constexpr (LAZY)
+          h = C.gather_ids(v, dv);
+        else
+          h = C.gather(v, dv);
         dv = rfl(dv);
         a = rfl(rdl(h.lx, 0));
         n_sdeg += (uint32_t)dv;
@@ -359,10 +367,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       // ---- weights of v's neighbourhood before / after the flip (commit and |B'|)
       uint32_t wo, wn;
       CSTAMP(-1);
-      C.template weights_old_new<MODE>(h, a, d, m, nbd, wo, wn);
       const bool mine = GRID ? lane <= 4 : lane <= dv;
-      const int plus = __popcll(ballot(mine && wo == 0 && wn > 0));
-      const int minus = __popcll(ballot(mine && wo > 0 && wn == 0));
+      int plus = 0, minus = 0;
+      if constexpr (!LAZY) {
+        C.template weights_old_new<MODE>(h, a, d, m, nbd, wo, wn);
+        plus = __popcll(ballot(mine && wo == 0 && wn > 0));
+        minus = __popcll(ballot(mine && wo > 0 && wn == 0));
+      }
       // ---- accept rule (include/flipwalk.h FW_ACCEPT_*)
       bool accepted;
       if (FULL && p.accept == FW_ACCEPT_BOUNDARY) {  // uniform_accept + boundary_condition
@@ -398,6 +409,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         pend = Pend{v, (int32_t)d, (uint32_t)t};
       }
       if (accepted) {
+        if constexpr (LAZY) {
+          int dv2;
+          h = C.gather(v, dv2);
+          C.template weights_old_new<MODE>(h, a, d, m, nbd, wo, wn);
+          plus = __popcll(ballot(mine && wo == 0 && wn > 0));
+          minus = __popcll(ballot(mine && wo > 0 && wn == 0));
+        }
         n_acc += 1;
         if (FULL && p.sched) sched_row(n_acc);
         n_adeg += (uint32_t)dv;
