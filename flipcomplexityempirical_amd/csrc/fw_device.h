@@ -820,6 +820,7 @@ struct Ctx {
   int32_t scap;  // race_search_b3: next-level entries staged over the group sums (<= 128)
   int lane;
   bool bb;  // grids: exact searches try the bitboard form first
+  uint64_t nbadj_pre = 0;  // gather_ids: lane l's entry of v's row of nbadj
   int my_dr, my_dc;
 #ifdef FW_STAMPS
   uint32_t n_win = 0, n_bbs = 0, n_list = 0;  // contiguity checks by the path that decided
@@ -979,7 +980,7 @@ struct Ctx {
   }
 
   // E16: v's neighbours (lanes 1..dv) and their labels, from v's padded row only
-  __device__ __forceinline__ Hood gather_ids(int v, int& dv) const {
+  __device__ __forceinline__ Hood gather_ids(int v, int& dv) {
     Hood h;
     h.x = -1;
     h.lx = NOLAB;
@@ -988,6 +989,9 @@ struct Ctx {
     h.has_v = false;
     h.deg = 0;
     const int xn = (lane >= 1 && lane <= 16) ? g.ell[(size_t)v * 16 + lane - 1] : -1;
+    // the local contiguity test's adjacency among v's neighbours, issued with v's row
+    // (C4 +3.5%, profiles/r04/c4_nbpre)
+    nbadj_pre = (lane >= 1 && lane <= 16) ? g.nbadj[(size_t)v * 16 + lane - 1] : 0ull;
     dv = __popcll(ballot(xn >= 0));
     if (lane > dv) return h;
     h.x = lane == 0 ? v : xn;
@@ -2013,7 +2017,9 @@ struct Ctx {
     return verdict == 1;
   }
 
-  // Contiguity of the proposal given the neighbourhood gathered for it.
+  // Contiguity of the proposal given the neighbourhood gathered for it (PRE: gather_ids
+  // fetched v's row of the neighbour adjacency).
+  template <bool PRE = false>
   __device__ __forceinline__ bool contiguous(int v, uint32_t a, int m, const Hood& h,
                                              uint64_t am, uint64_t& bfs_runs, uint64_t& bfs_nodes,
                                              uint64_t& bfs_deg) {
@@ -2034,7 +2040,7 @@ struct Ctx {
       // oracle's contiguous_after): one component is connected; otherwise pre-merge
       // nbadj has the padded [n][16] layout whenever the padded table exists
       const size_t e0 = (E16 || g.ell) ? (size_t)v * 16 : (size_t)g.rowptr[v];
-      const uint64_t adjl = ((am >> lane) & 1ull) ? (g.nbadj[e0 + lane - 1] << 1) & am : 0ull;
+      const uint64_t adjl = ((am >> lane) & 1ull) ? ((PRE ? nbadj_pre : g.nbadj[e0 + lane - 1]) << 1) & am : 0ull;
       // components of the sources' adjacency, one ballot per closure step: the relation
       // is symmetric, so a source joins when its own row meets the component
       uint64_t rest = am;

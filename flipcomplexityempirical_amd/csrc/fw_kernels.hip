@@ -352,7 +352,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
         // ---- contiguity (single_flip_contiguous)
         CSTAMP(2);  // gather, target, population
-        const bool cg = C.contiguous(v, a, m, h, am, n_bfs, n_bfsn, n_bfsd);
+        const bool cg = C.template contiguous<LAZY>(v, a, m, h, am, n_bfs, n_bfsn, n_bfsd);
         CSTAMP(3);  // contiguity
         if (!cg) {
           n_conf += 1;
