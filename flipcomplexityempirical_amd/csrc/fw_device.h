@@ -684,10 +684,9 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
       const uint32_t Db0 = (Fb0 | (Fb0 << 1) | (Fb0 >> 1) | (Fb1 << 31) | from_prev_lane(Fb0) | from_next_lane(Fb0)) & A0;
       const uint32_t Db1 = (Fb1 | (Fb1 << 1) | (Fb1 >> 1) | (Fb0 >> 31) | from_prev_lane(Fb1) | from_next_lane(Fb1)) & A1;
       const uint32_t nw0 = (Da0 | Db0) & ~V0, nw1 = (Da1 | Db1) & ~V1;
-      if (ballot(((Da0 & (Fb0 | (Db0 & nw0))) | (Da1 & (Fb1 | (Db1 & nw1)))) != 0u)) {
-        vd = 1;  // the two classes met: connected, the cells processed are V
-        break;
-      }
+      const bool met = ballot(((Da0 & (Fb0 | (Db0 & nw0))) | (Da1 & (Fb1 | (Db1 & nw1)))) != 0u) != 0ull;
+      // the state advances unconditionally and the loop has one exit (no per-exit copies
+      // of the loop-carried sets)
       Qa0 = Fa0;
       Qa1 = Fa1;
       Qb0 = Fb0;
@@ -696,12 +695,18 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
       Fa1 = Da1 & nw1;
       Fb0 = Db0 & nw0;
       Fb1 = Db1 & nw1;
-      if (!ballot((Fa0 | Fa1) != 0u) || !ballot((Fb0 | Fb1) != 0u)) {
-        vd = 0;  // a class reached no new cell: closed, disconnected
-        break;
-      }
       V0 |= nw0;
       V1 |= nw1;
+      const bool closed = !ballot((Fa0 | Fa1) != 0u) || !ballot((Fb0 | Fb1) != 0u);
+      if (met || closed) {
+        // met: the two classes met, connected; closed: a class reached no new cell,
+        // disconnected.  Either way the cells processed are the visited ones before this
+        // level's new cells.
+        vd = met ? 1 : 0;
+        V0 &= ~nw0;
+        V1 &= ~nw1;
+        break;
+      }
     }
     const uint32_t pc = (uint32_t)(__popc(V0) + __popc(V1));
     uint32_t dg = pc * (uint32_t)((r > 0) + (r < H - 1) + 2);
@@ -1420,6 +1425,7 @@ struct Ctx {
     // window-edge cells with an on-grid neighbour outside the window
     const bool e_top = lane == 0 && R0 > 0, e_bot = lane == 63 && R0 + 127 < H - 1;
     const bool e_left = C0 > 0, e_right = C0 + WC - 1 < W - 1;
+    int vd = -1;
     for (;;) {
       bool edge = false;
 #pragma unroll
@@ -1480,12 +1486,13 @@ struct Ctx {
         pb0 = b0;
         pb1 = b1;
       }
-      if (ballot(met) || !ballot(any_a) || !ballot(any_b)) {
-        // the two classes met: connected; or a class reached no new cell: closed
-        bfs_nodes += wave_sum(pc);
-        bfs_deg += wave_sum(pdeg);
-        return ballot(met) ? 1 : 0;
-      }
+      vd = ballot(met) ? 1 : (!ballot(any_a) || !ballot(any_b)) ? 0 : -1;
+      if (vd >= 0) break;  // the two classes met: connected; a class closed: disconnected
+    }
+    if (vd >= 0) {
+      bfs_nodes += wave_sum(pc);
+      bfs_deg += wave_sum(pdeg);
+      return vd;
     }
     // left the window: hand the race to the list search
 #ifdef FW_EXP1
