@@ -1568,10 +1568,15 @@ __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
   grid16_body<LB, MODE, PER, FULL, BIG, 1>(p);
 }
 
-// speculative attempts: R rows per chain, a 4-waves-per-SIMD register budget (128 VGPRs),
-// since it is used where chains are too few for the R = 1 kernel's 3 waves per SIMD
+// speculative attempts: R rows per chain.  A 3-waves-per-SIMD register budget (168 VGPRs:
+// 2-4 spilled, against ~60 under the 4-wave budget of round 3): C2 (4,096 chains, R = 4)
+// 1.256 -> 1.316 x 10^9, the 8,192-chain C3 shard R = 2 equal to R = 1
+// (profiles/r04/spec_wpe3/)
+#ifndef FW_SPEC_WPE
+#define FW_SPEC_WPE 3
+#endif
 template <int LB, int MODE, int PER, int R>
-__global__ __launch_bounds__(64 * MAX_NW) __attribute__((amdgpu_waves_per_eu(4))) void
+__global__ __launch_bounds__(64 * MAX_NW) __attribute__((amdgpu_waves_per_eu(FW_SPEC_WPE))) void
 fw_grid16_spec_kernel(FwRunParams p) {
   grid16_body<LB, MODE, PER, false, false, R>(p);
 }
@@ -1756,10 +1761,11 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
     }
     if (r_nw == 0) continue;
     const double e_r = R == 1 ? 1.0 : (R == 2 ? 1.56 : 1.0 + 0.56 + 0.56 * 0.56 + 0.56 * 0.56 * 0.56);
-    // per-row speed of the speculative kernels relative to R = 1 (their 128-VGPR budget
-    // spills ~60 VGPRs; the merge), calibrated on profiles/r03/e/ab_spec.jsonl: C2 (4,096
-    // chains) R = 4 +5..8% over R = 1, the 8,192-chain C3 shard R = 2 -1..-2.5%
-    const double eff = R == 1 ? 1.0 : (R == 2 ? 0.6 : 0.52);
+    // per-row speed of the speculative kernels relative to R = 1 (the merge, a few spilled
+    // VGPRs), calibrated on the measured lines: C2 (4,096 chains) R = 4 ~ +10% over R = 1
+    // and +1.5% over R = 2, the 8,192-chain C3 shard R = 2 equal to R = 1 and R = 4 -28%
+    // (profiles/r03/e/ab_spec.jsonl, profiles/r04/spec_wpe3/)
+    const double eff = R == 1 ? 1.0 : (R == 2 ? 0.6 : 0.72);
     const double waves = (double)r_blocks * r_nw * prop.multiProcessorCount;
     const double units = (double)((p.n_chains + cpw - 1) / cpw);
     const double score = std::min(units, waves) * cpw * e_r * eff;

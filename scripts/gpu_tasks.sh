@@ -16,6 +16,7 @@
 #   stamps_c5 / stamps_c4 per-phase clocks (stamps build) at the C5 checkpoint / C4
 #   steady                SURVEY 8d's steady state on every workload -> OUT/steady.jsonl
 #   ab:TAG:ARGS:LIB,LIB.. interleaved A/B of ab/lib_<LIB>.so builds (3 rounds) -> OUT/ab_TAG.jsonl
+#                         (LIB@VAR=VALUE: with one environment setting)
 #   multi                 bench.py under torch.distributed.run, 2 gloo ranks on device 0
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/$1
@@ -93,7 +94,10 @@ run_task() {
       args=${args//,/ }
       for rep in 1 2 3; do
         for v in ${libs//,/ }; do
-          FLIPWALK_LIB=$PWD/ab/lib_$v.so timeout -k 10 300 python -u bench.py $args --no-cpu-baseline > $O/one.json 2> $O/one.err || { echo "$v failed"; tail -5 $O/one.err; return 1; }
+          # a lib may carry one environment setting: name@VAR=VALUE
+          local lib=${v%%@*} envs=""
+          [ "$lib" != "$v" ] && envs=${v#*@}
+          env $envs FLIPWALK_LIB=$PWD/ab/lib_$lib.so timeout -k 10 300 python -u bench.py $args --no-cpu-baseline > $O/one.json 2> $O/one.err || { echo "$v failed"; tail -5 $O/one.err; return 1; }
           python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); pc=d.get('parity_check') or {}; print(json.dumps({'tag': sys.argv[4], 'lib': sys.argv[2], 'rep': int(sys.argv[3]), 'value': d['value'], 'kernel_ms': d['kernel_ms'], 'parity': [pc.get('equal'), pc.get('chains')]}))" $O/one.json $v $rep $tag | tee -a $O/ab_$tag.jsonl
         done
       done ;;
