@@ -67,6 +67,7 @@ run_task() {
     prof_c5:*)  # the same with the library ab/lib_<LIB>.so
       local lib=${t#prof_c5:}
       FLIPWALK_LIB=$PWD/ab/lib_$lib.so prof c5steady_$lib "--config c5 --shard 0/8 --resume $CK5 --check-chains 0" "--steps 5 --warmup 0 --inner 1000 --no-cpu-baseline --config c5 --shard 0/8 --resume $CK5 --check-chains 0" ;;
+    prof_c5fresh) prof c5fresh "--config c5 --shard 0/8" ;;
     prof_c4) prof c4 "--config c4" ;;
     prof_c4r) prof c4r "--config c4 --order random" ;;
     prof_frank) prof frank "--config frank" ;;
