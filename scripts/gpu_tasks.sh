@@ -102,6 +102,12 @@ run_task() {
           python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); pc=d.get('parity_check') or {}; print(json.dumps({'tag': sys.argv[4], 'lib': sys.argv[2], 'rep': int(sys.argv[3]), 'value': d['value'], 'kernel_ms': d['kernel_ms'], 'parity': [pc.get('equal'), pc.get('chains')]}))" $O/one.json $v $rep $tag | tee -a $O/ab_$tag.jsonl
         done
       done ;;
+    shards_c5)  # the 8-GPU C5 job emulated shard by shard at the steady-state protocol
+      timeout -k 10 900 bash scripts/shards.sh 8 "--config c5 --steps 100 --warmup 10 --check-chains 2" c5 > $O/shards_c5.log 2>&1 || { tail -5 $O/shards_c5.log; return 1; }
+      tail -10 $O/shards_c5.log ;;
+    shards_c3)  # the 8-GPU C3 job emulated shard by shard on the driver protocol
+      timeout -k 10 600 bash scripts/shards.sh 8 "--config c3 --steps 20 --warmup 5 --check-chains 2" c3 > $O/shards_c3.log 2>&1 || { tail -5 $O/shards_c3.log; return 1; }
+      tail -10 $O/shards_c3.log ;;
     multi)
       timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --config c3 --chains 8192 --steps 2 --warmup 1 --backend gloo --same-device --no-cpu-baseline --check-chains 4 > $O/multi.json 2> $O/multi.err || { tail -20 $O/multi.err; return 1; }
       tail -1 $O/multi.json ;;
