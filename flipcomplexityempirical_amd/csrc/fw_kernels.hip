@@ -725,48 +725,51 @@ int fw_run_grid_size(FwRunParams& p, int lb, int device, int* grid) {
   // down to 128 entries (longer searches continue in the HBM spill area), when that keeps
   // one more chain per CU; the longest list that reaches the best residency is kept.
   // FLIPWALK_LIST_CAP pins the length (tests of the spill path).
-  // With 3-bit labels the list search (a rare fallback past the bitboard window) keeps its
-  // marks in HBM anyway, and the list may shrink to 8 entries.
+  // With 3- or 5-bit labels the list search (a rare fallback) keeps its marks in HBM or in
+  // the labels anyway, and the list may shrink to 8 entries.
+  // 4- and 5-bit labels on padded rows also weigh the 5-waves-per-SIMD instantiation (the
+  // Frankengraph: 16 -> 20 chains per CU, +4%), taken when it holds more chains per CU; the
+  // list length is chosen together with it (C4 with its LDS weights: 17 chains per CU at
+  // the 256-entry list, 19 at 8 entries).  FLIPWALK_NO_WPE5=1 keeps the 4-wave budget (A/B).
   const char* cap_env = getenv("FLIPWALK_LIST_CAP");
   const int q_min = lb == 3 || lb == 5 ? 8 : 128;
-  if (!(cap_env && cap_env[0]) && p.qcap > q_min) {
+  const char* no5 = getenv("FLIPWALK_NO_WPE5");
+  void* fn5 = (lb == 4 || lb == 5) && p.g.gw == 0 && p.g.ell != nullptr && !(no5 && no5[0] == '1')
+                  ? pick_run(lb, false, true, p.mode, p.G, true, true, p.wb != 0)
+                  : nullptr;
+  auto occ = [&](void* f, int lds, int& pc) -> bool {
+    pc = 0;
+    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess &&
+           hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, f, 64, (size_t)lds) == hipSuccess;
+  };
+  {
+    const bool pinned = (cap_env && cap_env[0]) || p.qcap <= q_min;
     const int base = p.off_list;
-    int best_q = p.qcap, best = per_cu;
-    for (int q = p.qcap - 8; q >= q_min; q -= 8) {
+    int best_q = p.qcap, best = 0;
+    bool best5 = false;
+    for (int q = p.qcap; q >= (pinned ? p.qcap : q_min); q -= 8) {
       const int lds = base + 4 * q;
-      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-        return -1;
-      int pc = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, fn, 64, (size_t)lds) != hipSuccess)
-        return -1;
-      if (pc > best) {
-        best = pc;
+      int pc4 = 0, pc5 = 0;
+      if (!occ(fn, lds, pc4)) return -1;
+      if (fn5 && !occ(fn5, lds, pc5)) return -1;
+      if (pc4 > best) {
+        best = pc4;
         best_q = q;
+        best5 = false;
+      }
+      if (pc5 > best) {
+        best = pc5;
+        best_q = q;
+        best5 = true;
       }
     }
+    if (best <= 0) return -1;
     p.qcap = best_q;
     p.lds_bytes = base + 4 * best_q;
+    p.wpe5 = best5 ? 1 : 0;
     per_cu = best;
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
-        hipSuccess)
-      return -1;
-  }
-  // 4-bit labels on padded rows: when LDS admits more chains per CU than the 4-wave
-  // register budget, the 5-wave instantiation (Frankengraph: 16 -> 20 chains per CU, +4%)
-  p.wpe5 = 0;
-  if ((lb == 4 || lb == 5) && p.g.gw == 0 && p.g.ell != nullptr) {
-    void* fn5 = pick_run(lb, false, true, p.mode, p.G, true, true, p.wb != 0);
-    if (hipFuncSetAttribute(fn5, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes) !=
-        hipSuccess)
-      return -1;
-    int pc5 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc5, fn5, 64, (size_t)p.lds_bytes) !=
-        hipSuccess)
-      return -1;
-    if (pc5 > per_cu) {
-      p.wpe5 = 1;
-      per_cu = pc5;
-    }
+    int dummy = 0;
+    if (!occ(fn, p.lds_bytes, dummy) || (fn5 && !occ(fn5, p.lds_bytes, dummy))) return -1;
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
