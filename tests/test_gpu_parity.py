@@ -403,6 +403,35 @@ def test_bitboard_window_escape(gpu_lib, k, vertical, path, monkeypatch):
     assert (st["bfs_nodes"] > 40 * st["bfs_runs"]).any()  # searches far past the window
 
 
+@pytest.mark.parametrize("vertical", [False, True])
+def test_bitboard_128_escape_3bit(gpu_lib, vertical, monkeypatch):
+    """3-bit labels (the C5 path): a race along a corridor longer than 128 cells leaves the
+    64 x 64 bitboard, continues on the 128 x 128 stage (race_bb4), leaves that too and ends
+    in the list search seeded with the 128 window's last two levels.  Plans and every search
+    counter against the oracle, chain by chain."""
+    from flipcomplexityempirical_amd.chain import metropolis_table
+    from flipcomplexityempirical_amd.graph import grid_graph
+    monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
+    monkeypatch.setenv("FLIPWALK_CSR_LB", "3")
+    monkeypatch.delenv("FLIPWALK_NO_BITBOARD", raising=False)
+    h, w, k = 30, 300, 6
+    g = grid_graph(w, h) if vertical else grid_graph(h, w)
+    init = _corridor_plan(h, w, k, vertical)
+    assert O.plan_valid(g, init, k, 1, g.n)
+    dg = DeviceGraph(g)
+    thr = metropolis_table(1.0, g.maxdeg)
+    n_chains, steps, seed = 21, 120, 9
+    ch = Chains(dg, n_chains, k, init, proposal="pairs", pop_bounds=(1, g.n), base=1.0, seed=seed)
+    ch.run(steps)
+    labs, st = ch.labels(), ch.stats()
+    for i in range(n_chains):
+        olab, ost, _, _ = O.run_chain(g, init, k, 1, 1, g.n, thr, seed, i, steps)
+        assert np.array_equal(labs[i], olab), i
+        for f in ("attempts", "steps", "accepts", "contig_fail", "bfs_runs", "bfs_nodes", "bfs_deg"):
+            assert int(st[f][i]) == int(ost[f][0]), (i, f, st[f][i], ost[f][0])
+    assert (st["bfs_nodes"] > 150 * st["bfs_runs"]).any()  # searches far past 128 cells
+
+
 @pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
                                        ("sec11_a2_k2", "auto"), ("tract_k4", "auto")])
 def test_counter_fold_bit_exact(gpu_lib, name, path, monkeypatch):

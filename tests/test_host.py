@@ -152,3 +152,26 @@ def test_bench_refuses_maps_with_resume():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--maps", "--resume",
                         "x.npz"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "--maps cannot be combined with --resume" in r.stderr
+
+
+def test_hilbert_numbering_is_the_same_graph():
+    """delaunay_graph(order="hilbert") renumbers the C4 graph along the Hilbert curve of its
+    points: the same graph up to isomorphism (the same points, populations and triangles),
+    with neighbours mostly in the same 64-node weight group."""
+    from flipcomplexityempirical_amd.graph import delaunay_graph, hilbert_index
+    g0, g1 = delaunay_graph(2000, seed=3), delaunay_graph(2000, seed=3, order="hilbert")
+    assert (g0.n, g0.n_edges, g0.total_pop) == (g1.n, g1.n_edges, g1.total_pop)
+    # map by point coordinates: the edge sets agree
+    pos0 = {(a["x"], a["y"]): i for i, a in enumerate(g0.node_attrs)}
+    perm = np.array([pos0[(a["x"], a["y"])] for a in g1.node_attrs])
+    e1 = {tuple(sorted((int(perm[u]), int(perm[v])))) for u, v in g1.edges()}
+    e0 = {tuple(map(int, e)) for e in g0.edges()}
+    assert e0 == e1
+    assert np.array_equal(g1.pop, g0.pop[perm])
+    src = np.repeat(np.arange(g1.n), g1.degrees)
+    assert ((src // 64) == (g1.col // 64)).mean() > 0.6
+    # the curve visits a 4 x 4 lattice cell by cell
+    side = 4
+    xy = np.array([[(i + .5) / side, (j + .5) / side] for i in range(side) for j in range(side)])
+    walk = (xy[np.argsort(hilbert_index(xy, 2))] * side).astype(int)
+    assert all(np.abs(walk[i] - walk[i + 1]).sum() == 1 for i in range(15))
