@@ -74,6 +74,8 @@ run_task() {
     prof_c3) prof c3 "" ;;
     prof_c2) prof c2 "--config c2" ;;
     prof_c3s8) prof c3s8 "--config c3 --shard 0/8" ;;
+    prof_c3s4) prof c3s4 "--config c3 --shard 0/4" ;;
+    prof_c3s2) prof c3s2 "--config c3 --shard 0/2" ;;
     stamps_c5)
       timeout -k 10 300 python -u scripts/stamps.py c5 8192 1 $CK5 > $O/stamps_c5_100k.txt 2>&1 || { tail -5 $O/stamps_c5_100k.txt; return 1; }
       grep -v amdgpu.ids $O/stamps_c5_100k.txt ;;
