@@ -2064,6 +2064,7 @@ struct Ctx {
         for (uint64_t t = comp & (comp - 1ull); t; t &= t - 1ull)
           merge(sx(L0), sx(__ffsll((unsigned long long)t) - 1));
       }
+      CTX_LAP(c_win);  // stamps: the local test's cycles of the searches it did not decide
     }
     if constexpr (GRID) {
       const uint64_t rb = ballot(lane >= 1 && lane <= 8 && h.lx == a) >> 1;
@@ -2146,7 +2147,7 @@ struct Ctx {
       verdict = race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else
       verdict = race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);
-    if constexpr (GRID) CTX_LAP(c_list);
+    CTX_LAP(c_list);
     return verdict;
   }
 };
