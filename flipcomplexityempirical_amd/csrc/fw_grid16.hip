@@ -1731,6 +1731,8 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
   const char* es = getenv("FLIPWALK_SPEC");
   const int force = es && es[0] ? atoi(es) : 0;
+  const char* en = getenv("FLIPWALK_GRID16_NW");  // force the waves per workgroup
+  const int force_nw = en && en[0] ? atoi(en) : 0;
   const bool full = grid16_full(p);
   const bool spec_ok = !big && (p.lb == 2 || p.lb == 4) && !full;
   double best_score = -1.0;
@@ -1741,10 +1743,23 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
     void* fn = grid16_fn_r(p, full, R);
     if (!fn) return -1;
     const int cpw = 4 / R;
-    // waves per workgroup for this R: the most resident waves per CU (ties: fewer)
+    // waves per workgroup for this R: the most resident waves per CU (ties: fewer).  With
+    // fewer waves of work than resident slots (the 8-GPU job's 8,192-chain shards) the
+    // busiest SIMD sets the launch time: the workgroups are dealt evenly over the CUs and a
+    // CU's waves over its four SIMDs, so the pick is the fewest waves on the busiest SIMD
+    // (3-wave workgroups put 683 of them on 256 CUs: 3, 2, 2, 2 waves; 4-wave ones 2 each).
+    const long long wunits = (p.n_chains + cpw - 1) / cpw;
+    const int cus = prop.multiProcessorCount;
+    auto busiest_simd = [&](int nw, int per_cu) -> long long {
+      const long long wgs = (wunits + nw - 1) / nw;
+      if (wgs > (long long)per_cu * cus) return -1;  // more work than slots: rounds
+      return ((wgs + cus - 1) / cus * nw + 3) / 4;
+    };
     int r_nw = 0, r_blocks = 0, r_lds = 0;
+    long long r_busy = -1;
     for (int nw = R; nw <= MAX_NW; ++nw) {
       if (nw % R) continue;  // the R = 1 kernels must fill the same slots (fw_grid16_launch_nw)
+      if (force_nw && nw != force_nw) continue;
       const int lds = LDS_GUARD + cpw * nw * stride + p.scr_bytes + 4 * p.qcap16;
       if (lds > 160 * 1024 - 256) break;
       if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
@@ -1753,10 +1768,21 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nw, (size_t)lds) !=
           hipSuccess)
         return -1;
-      if (per_cu * nw > r_blocks * r_nw) {
+      const long long busy = per_cu > 0 ? busiest_simd(nw, per_cu) : -1;
+      bool take;
+      if (r_nw == 0)
+        take = per_cu > 0;
+      else if (busy >= 0 && r_busy >= 0)  // both hold all the work: the less loaded SIMD
+        take = busy < r_busy || (busy == r_busy && per_cu * nw > r_blocks * r_nw);
+      else if (busy >= 0 || r_busy >= 0)  // only one holds all the work
+        take = busy >= 0;
+      else
+        take = per_cu * nw > r_blocks * r_nw;
+      if (take) {
         r_nw = nw;
         r_blocks = per_cu;
         r_lds = lds;
+        r_busy = busy;
       }
     }
     if (r_nw == 0) continue;
