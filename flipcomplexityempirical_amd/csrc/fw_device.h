@@ -592,7 +592,8 @@ struct BBSeed {
 template <int LB>
 __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int lane, int vr,
                              int vc, uint32_t a, uint32_t am4, uint32_t lk, uint64_t& bfs_nodes,
-                             uint64_t& bfs_deg, BBSeed& sd) {
+                             uint64_t& bfs_deg, BBSeed& sd, uint32_t& lv_mid,
+                             uint32_t& lv_64) {
   sd.ok = false;
   const int r = vr - 32 + lane, c0 = vc - 32;
   const bool rin = (r >= 0) & (r < H);
@@ -665,8 +666,52 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
     }
     uint32_t Qa0 = 0u, Qa1 = 0u, Qb0 = 0u, Qb1 = 0u;  // the previous level, per class
     uint32_t V0 = Fa0 | Fb0, V1 = Fa1 | Fb1;
-    int vd;
-    for (;;) {
+    int vd = -1;
+#ifndef FW_NO_MID32
+    {
+      // The race starts on the window's middle 32 columns (vc - 16 .. vc + 15, one VGPR per
+      // set: half the work per level) and moves to the 64 columns with its state when a
+      // frontier reaches that strip's edge.  The levels are the same: a frontier clear of
+      // the strip's edge dilates inside it.
+      auto mid = [](uint32_t x0, uint32_t x1) { return (x0 >> 16) | (x1 << 16); };
+      const uint32_t am = mid(A0, A1);
+      uint32_t em = er;
+      if (c0 + 16 > 0) em |= 1u;
+      if (c0 + 47 < W - 1) em |= 1u << 31;
+      em &= am;
+      uint32_t fa = mid(Fa0, Fa1), fb = mid(Fb0, Fb1), qa = 0u, qb = 0u, vv = fa | fb;
+      for (;;) {
+        if (ballot(((fa | fb) & em) != 0u)) break;  // on to the 64 columns
+        ++lv_mid;
+        const uint32_t da = (fa | (fa << 1) | (fa >> 1) | from_prev_lane(fa) | from_next_lane(fa)) & am;
+        const uint32_t db = (fb | (fb << 1) | (fb >> 1) | from_prev_lane(fb) | from_next_lane(fb)) & am;
+        const uint32_t nw = (da | db) & ~vv;
+        const bool met = ballot((da & (fb | (db & nw))) != 0u) != 0ull;
+        qa = fa;
+        qb = fb;
+        fa = da & nw;
+        fb = db & nw;
+        vv |= nw;
+        const bool closed = !ballot(fa != 0u) || !ballot(fb != 0u);
+        if (met || closed) {
+          vd = met ? 1 : 0;
+          vv &= ~nw;
+          break;
+        }
+      }
+      Qa0 = qa << 16;
+      Qa1 = qa >> 16;
+      Qb0 = qb << 16;
+      Qb1 = qb >> 16;
+      Fa0 = fa << 16;
+      Fa1 = fa >> 16;
+      Fb0 = fb << 16;
+      Fb1 = fb >> 16;
+      V0 = vv << 16;
+      V1 = vv >> 16;
+    }
+#endif
+    if (vd < 0) for (;;) {
       if (ballot((((Fa0 | Fb0) & E0) | ((Fa1 | Fb1) & E1)) != 0u)) {
         // processed cells (levels < L) and their degrees, counted as the list search counts
         // its dequeued nodes
@@ -679,6 +724,7 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
         sd = BBSeed{Qa0, Qa1, Qb0, Qb1, Fa0, Fa1, Fb0, Fb1, pc, dg, ra, rb, true};
         return -1;
       }
+      ++lv_64;
       const uint32_t Da0 = (Fa0 | (Fa0 << 1) | (Fa0 >> 1) | (Fa1 << 31) | from_prev_lane(Fa0) | from_next_lane(Fa0)) & A0;
       const uint32_t Da1 = (Fa1 | (Fa1 << 1) | (Fa1 >> 1) | (Fa0 >> 31) | from_prev_lane(Fa1) | from_next_lane(Fa1)) & A1;
       const uint32_t Db0 = (Fb0 | (Fb0 << 1) | (Fb0 >> 1) | (Fb1 << 31) | from_prev_lane(Fb0) | from_next_lane(Fb0)) & A0;
@@ -833,6 +879,8 @@ struct Ctx {
   uint64_t n_bbl = 0;                          // bitboard levels run (decided or escaped)
   uint64_t n_lvl = 0, c_clear = 0;  // race_search_b3: levels, restore cycles
   uint64_t n_mapt = 0, n_seed = 0;  // rounds of map tests; searches seeded by the bitboard
+  uint64_t n_lv_mid = 0, n_lv_64 = 0;  // grid_race_bb2 levels on 32 / 64 columns
+  uint64_t n_bb4 = 0, c_bb4 = 0;       // race_bb4 runs and their cycles
   __device__ static __forceinline__ uint64_t now() {
     uint64_t t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1422,6 +1470,23 @@ struct Ctx {
         if (pos >= 32 * d) dd = f[d];
       return (dd >> (pos & 31)) & 1u;
     };
+    // The processed cells are counted once, after the loop: they are the frontier handed
+    // over plus the cells reached since, less the current frontier, i.e. per row
+    // |F0| + |U0| - |U| - |F| (F0, U0 disjoint; U only shrinks), and a grid-edge column's
+    // cell is processed when it was in F0 | U0 and is in neither U nor F now.
+    uint32_t cnt[2], ebits = 0u;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint32_t f[ND];
+      cnt[p] = 0u;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        f[d] = Fa[p][d] | Fb[p][d] | U[p][d];
+        cnt[p] += (uint32_t)__popc(f[d]);
+      }
+      if (w0 >= 0 && w0 < WC) ebits |= wbit(f, w0) << (2 * p);
+      if (w1 >= 0 && w1 < WC) ebits |= wbit(f, w1) << (2 * p + 1);
+    }
     // window-edge cells with an on-grid neighbour outside the window
     const bool e_top = lane == 0 && R0 > 0, e_bot = lane == 63 && R0 + 127 < H - 1;
     const bool e_left = C0 > 0, e_right = C0 + WC - 1 < W - 1;
@@ -1437,22 +1502,6 @@ struct Ctx {
         if (p == 0 ? e_top : e_bot) edge |= any != 0u;
       }
       if (ballot(edge)) break;
-      // this level's frontier is processed: count it
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        uint32_t f[ND];
-        uint32_t c = 0;
-#pragma unroll
-        for (int d = 0; d < ND; ++d) {
-          f[d] = Fa[p][d] | Fb[p][d];
-          c += (uint32_t)__popc(f[d]);
-        }
-        pc += c;
-        uint32_t dg = c * (p == 0 ? fdeg0 : fdeg1);
-        if (w0 >= 0 && w0 < WC) dg -= wbit(f, w0);
-        if (w1 >= 0 && w1 < WC) dg -= wbit(f, w1);
-        pdeg += dg;
-      }
       // dilations, the new cells and the merge test, one column of dwords at a time (both
       // rows), updating the sets in place: the old values a later dword needs (its left
       // neighbour's carry) are held in pa / pb, and the other lanes' rows are read by DPP
@@ -1488,6 +1537,21 @@ struct Ctx {
       }
       vd = ballot(met) ? 1 : (!ballot(any_a) || !ballot(any_b)) ? 0 : -1;
       if (vd >= 0) break;  // the two classes met: connected; a class closed: disconnected
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint32_t f[ND];
+      uint32_t c = cnt[p];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        f[d] = Fa[p][d] | Fb[p][d] | U[p][d];
+        c -= (uint32_t)__popc(f[d]);
+      }
+      uint32_t dg = c * (p == 0 ? fdeg0 : fdeg1);
+      if (w0 >= 0 && w0 < WC) dg -= ((ebits >> (2 * p)) & 1u) & (wbit(f, w0) ^ 1u);
+      if (w1 >= 0 && w1 < WC) dg -= ((ebits >> (2 * p + 1)) & 1u) & (wbit(f, w1) ^ 1u);
+      pc += c;
+      pdeg += dg;
     }
     if (vd >= 0) {
       bfs_nodes += wave_sum(pc);
@@ -2098,8 +2162,14 @@ struct Ctx {
         int wv;
         if constexpr (LB == 3) {
           BBSeed s2;
+          uint32_t lv_mid = 0, lv_64 = 0;
           wv = grid_race_bb2<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk, bfs_nodes,
-                                 bfs_deg, s2);
+                                 bfs_deg, s2, lv_mid, lv_64);
+#ifdef FW_STAMPS
+          n_lv_mid += lv_mid;
+          n_lv_64 += lv_64;
+#endif
+          CTX_LAP(c_bbs);
           if (s2.ok) {  // the classes' source indices (CSR order of v's neighbours)
             s2.ra = sx(s2.ra + 1);
             s2.rb = sx(s2.rb + 1);
@@ -2107,6 +2177,10 @@ struct Ctx {
 #define FW_BB4_ND 4
 #endif
             wv = race_bb4<FW_BB4_ND>(v, vr, vc, a, m, s2, bfs_nodes, bfs_deg, rs);
+#ifdef FW_STAMPS
+            n_bb4 += 1;
+#endif
+            CTX_LAP(c_bb4);
           }
         } else {
           wv = grid_race_bb<LB>(lab, g.n, g.gw, g.gh, lane, vr, vc, a, am4, lk, bfs_nodes,

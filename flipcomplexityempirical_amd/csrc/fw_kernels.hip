@@ -32,8 +32,8 @@
 #ifdef FW_STAMPS
 // Diagnostic build only (libflipwalk_stamps.so): per-phase s_memtime shares of the
 // one-chain-per-wave kernel (scripts/stamps.py --csr).
-__device__ unsigned long long g_stamps_csr[16];
-#define CSTAMP_DECL uint64_t st_acc[16] = {}; uint64_t st_t0 = 0;
+__device__ unsigned long long g_stamps_csr[24];
+#define CSTAMP_DECL uint64_t st_acc[24] = {}; uint64_t st_t0 = 0;
 #define CSTAMP(i)                                             \
   do {                                                        \
     __builtin_amdgcn_sched_barrier(0);                        \
@@ -46,7 +46,7 @@ __device__ unsigned long long g_stamps_csr[16];
 #define CSTAMP_COUNT(i, v) st_acc[i] += (uint64_t)(v)
 #define CSTAMP_FLUSH                                          \
   if (__lane_id() == 0)                                       \
-    for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_stamps_csr[i_], (unsigned long long)st_acc[i_]);
+    for (int i_ = 0; i_ < 24; ++i_) atomicAdd(&g_stamps_csr[i_], (unsigned long long)st_acc[i_]);
 #else
 #define CSTAMP_DECL
 #define CSTAMP(i)
@@ -515,6 +515,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   CSTAMP_COUNT(7, C.n_seed);
   CSTAMP_COUNT(14, C.c_clear);
   CSTAMP_COUNT(15, C.n_mapt);
+  CSTAMP_COUNT(16, C.n_lv_mid);
+  CSTAMP_COUNT(17, C.n_lv_64);
+  CSTAMP_COUNT(18, C.n_bb4);
+  CSTAMP_COUNT(19, C.c_bb4);
 #endif
   CSTAMP_FLUSH
 }
@@ -639,10 +643,10 @@ __global__ void fw_map_read_kernel(FwMapRead m) {
 
 #ifdef FW_STAMPS
 extern "C" int fw_debug_stamps_csr(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_csr), sizeof(unsigned long long) * 16) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_csr), sizeof(unsigned long long) * 24) != hipSuccess)
     return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[24] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_csr), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

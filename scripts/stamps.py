@@ -35,7 +35,8 @@ for _ in range(int(sys.argv[3]) if len(sys.argv) > 3 else 2):
 buf = np.zeros(16, np.uint64)
 L.fw_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), 1)
 L.fw_debug_stamps_csr.argtypes = [ctypes.c_void_p, ctypes.c_int]
-L.fw_debug_stamps_csr(buf.ctypes.data_as(ctypes.c_void_p), 1)
+cz = np.zeros(24, np.uint64)
+L.fw_debug_stamps_csr(cz.ctypes.data_as(ctypes.c_void_p), 1)
 att0 = int(ch.stats()["attempts"].sum())
 for _ in range(3):
     ch.run(1000)
@@ -53,7 +54,7 @@ for nm, v in zip(names, buf):
 
 # the one-chain-per-wave kernel's stamps (configurations routed to it, e.g. C4, C5)
 L.fw_debug_stamps_csr.argtypes = [ctypes.c_void_p, ctypes.c_int]
-cb = np.zeros(16, np.uint64)
+cb = np.zeros(24, np.uint64)
 L.fw_debug_stamps_csr(cb.ctypes.data_as(ctypes.c_void_p), 0)
 if cb[:6].sum():
     att = int(st["attempts"].sum()) - att0
@@ -74,3 +75,8 @@ if cb[:6].sum():
               f"{cb[11] / att:.0f} / {cb[11] / max(cb[8], 1):.0f}, bitboard {cb[12] / att:.0f} / "
               f"{cb[12] / max(cb[9], 1):.0f}, list search {cb[13] / att:.0f} / "
               f"{cb[13] / max(cb[10], 1):.0f}")
+    if cb[16] + cb[17] + cb[18]:
+        bbs = max(int(cb[9]), 1)
+        print(f"64-row bitboard (two-class path): {cb[16] / bbs:.1f} levels on 32 columns, "
+              f"{cb[17] / bbs:.1f} on 64 per run; 128-wide stage: {cb[18] / att:.4f} runs per "
+              f"attempt, {cb[19] / max(cb[18], 1):.0f} clk per run ({cb[19] / att:.0f} per attempt)")
