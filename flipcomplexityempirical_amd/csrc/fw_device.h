@@ -401,10 +401,14 @@ __device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int
 #pragma unroll
   for (int j = 0; j <= LB; ++j) wd[j] = w[min(max(wi + j, 0), wlast)];
   if constexpr (LB == 3) {
-    // realign the 96 bits of the 32 fields to bit 0, then one field per bit-field extract
+    // realign the 96 bits of the 32 fields to bit 0; XOR with a repeated every 3 bits, so
+    // a field equals a iff its 3 bits are 0; OR each field's bits onto its lowest (funnel
+    // shifts carry the two fields that straddle words); then the fields' low bits, at
+    // stride 3 in each word (phases 0, 1, 2), are compacted as a 3-D Morton decode does
     const uint32_t r0 = __builtin_amdgcn_alignbit(wd[1], wd[0], sh);
     const uint32_t r1 = __builtin_amdgcn_alignbit(wd[2], wd[1], sh);
     const uint32_t r2 = __builtin_amdgcn_alignbit(wd[3], wd[2], sh);
+#ifdef FW_EQ3_SCALAR
     uint32_t out3 = 0;
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
@@ -423,6 +427,21 @@ __device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int
       out3 |= (f == a ? 1u : 0u) << j;
     }
     return out3;
+#else
+    const uint32_t pa = a * 0x49249249u;
+    const uint32_t y0 = r0 ^ pa, y1 = r1 ^ ((pa << 1) | (a >> 2)), y2 = r2 ^ ((pa << 2) | (a >> 1));
+    const uint32_t z0 = y0 | __builtin_amdgcn_alignbit(y1, y0, 1) | __builtin_amdgcn_alignbit(y1, y0, 2);
+    const uint32_t z1 = y1 | __builtin_amdgcn_alignbit(y2, y1, 1) | __builtin_amdgcn_alignbit(y2, y1, 2);
+    const uint32_t z2 = y2 | (y2 >> 1) | (y2 >> 2);
+    auto compact3 = [](uint32_t x) {  // bits 0, 3, ..., 30 -> 0 .. 10
+      x &= 0x49249249u;
+      x = (x ^ (x >> 2)) & 0xC30C30C3u;
+      x = (x ^ (x >> 4)) & 0x0F00F00Fu;
+      x = (x ^ (x >> 8)) & 0xFF0000FFu;
+      return (x ^ (x >> 16)) & 0x000007FFu;
+    };
+    return compact3(~z0) | (compact3(~z1 >> 1) << 11) | ((compact3(~z2 >> 2) & 0x3FFu) << 22);
+#endif
   }
   uint32_t out = 0;
 #pragma unroll
