@@ -220,14 +220,21 @@ def flipwalk_env():
 
 
 # ------------------------------------------------------------------ PMC profiles
-def pmc_key(config, order, chains, inner, steady):
-    """Name of the PMC summary of a workload (profiles/pmc/<key>.json): configuration, chains
-    on this GPU, steps per launch, and whether the chains were resumed at the steady state."""
+def pmc_key(config, order, chains, inner, warmup, steps, chain_id0=0, resumed=0):
+    """Name of the PMC summary of one bench protocol (profiles/pmc/<key>.json): workload,
+    chains on this GPU (and the first global id when it is a shard other than the first),
+    steps per launch, warm-up and timed launches, and the counted steps per chain a
+    --resume checkpoint already held (the steady state)."""
     from flipcomplexityempirical_amd.workloads import C4_ORDER
     name = config
     if config == "c4" and (order or C4_ORDER) != "hilbert":
         name += "r"
-    return f"{name}_{chains}_{inner}" + ("_steady" if steady else "")
+    key = f"{name}_{chains}_{inner}_w{warmup}_s{steps}"
+    if chain_id0:
+        key += f"_id{chain_id0}"
+    if resumed:
+        key += f"_r{resumed}"
+    return key
 
 
 def load_pmc(pmc_dir, key):
@@ -236,6 +243,27 @@ def load_pmc(pmc_dir, key):
         return None
     with open(path) as f:
         return json.load(f)
+
+
+def pmc_mismatch(prof, identity, kernel_ms, tol=0.10):
+    """Why a stored PMC profile does not describe this line (None when it does): it must
+    come from the same workload, protocol, FLIPWALK_* settings and library build, and its
+    timed launches' rocprof kernel time must be within ``tol`` of this line's HIP-event
+    kernel time (otherwise its per-launch counters describe other launches)."""
+    if prof is None:
+        return "no PMC profile of this protocol (profiles/pmc, scripts/profile.sh)"
+    pid = prof.get("identity")
+    if not pid:
+        return f"profile {prof.get('source')} carries no identity (an older protocol)"
+    diff = sorted(k for k in set(pid) | set(identity) if pid.get(k) != identity.get(k))
+    if diff:
+        return (f"profile {prof.get('source')} is of another configuration: "
+                + ", ".join(f"{k}={pid.get(k)!r} here {identity.get(k)!r}" for k in diff))
+    pms = (prof.get("kernel_trace") or {}).get("avg_ms")
+    if not pms or abs(pms - kernel_ms) > tol * kernel_ms:
+        return (f"profile {prof.get('source')} timed launches at {pms} ms (rocprof) vs this "
+                f"line's {kernel_ms:.4g} ms: more than {tol:.0%} apart")
+    return None
 
 
 # ------------------------------------------------------------------ main
@@ -299,16 +327,19 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # a process group whenever torch.distributed.run launched us, also at world 1 (the RCCL
+    # path then runs its collectives over one rank: tests/test_distributed.py)
+    launched = "MASTER_ADDR" in os.environ and "WORLD_SIZE" in os.environ
     shard_rank, shard_world = rank, world
     if args.shard:
-        if world > 1:
+        if launched:
             raise SystemExit("--shard emulates one rank of a job: run it as a single process")
         shard_rank, shard_world = (int(x) for x in args.shard.split("/"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = 0 if args.same_device else local_rank
     import torch
     dist = None
-    if world > 1:
+    if launched:
         import torch.distributed as dist
         torch.cuda.set_device(device)
         dist.init_process_group(args.backend)
@@ -413,21 +444,35 @@ def main():
     kernel_ms = float(np.mean(kms))
     bytes_per_launch = algorithmic_bytes(d) / args.steps
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    from flipcomplexityempirical_amd._lib import build_info
+    identity = {
+        "config": args.config, "order": args.order, "grid": args.grid, "k": k,
+        "proposal": proposal, "base": base_desc, "percent": percent, "seed": args.seed,
+        "chains": chains, "chain_id0": lo, "world": world, "inner": args.inner,
+        "warmup": args.warmup, "steps": args.steps, "resumed_steps": resumed,
+        "maps": bool(args.maps), "flipwalk_env": flipwalk_env(), "build": build_info(),
+    }
     prof = load_pmc(args.pmc_dir, pmc_key(args.config, args.order, chains, args.inner,
-                                          bool(args.resume)))
+                                          args.warmup, args.steps, lo, resumed))
+    why = pmc_mismatch(prof, identity, kernel_ms)
+    pmc_from = prof.get("source") if prof else None
+    if why:
+        prof = None  # its counters would describe other launches: every PMC field null
     traffic = prof.get("hbm_bytes_per_launch") if prof else None
     issue = None
     if prof and prof.get("valu_insts_per_launch"):
         # what binds this kernel: VALU issue.  Peak: every SIMD takes one wave64 VALU
         # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md) -> 256 CUs x 4 SIMDs
-        # x 2.4 GHz / 2; achieved: the PMC pass's VALU wave-instructions per launch
-        # over this run's mean launch time.
+        # x 2.4 GHz / 2; achieved: the PMC pass's VALU wave-instructions per timed launch
+        # over this run's mean launch time (the same protocol, pmc_mismatch).
         peak = 256 * 4 * 2.4e9 / 2
         ach = prof["valu_insts_per_launch"] / (kernel_ms * 1e-3)
         issue = {"bound": "valu-issue", "achieved": ach, "peak": peak,
                  "unit": "wave-instr/s", "frac": ach / peak, "source": prof.get("source"),
-                 # rocprofv3 --kernel-trace --stats mean of the same kernel, same command
-                 "rocprof_kernel_ms": (prof.get("kernel_trace") or {}).get("avg_ms")}
+                 # rocprofv3 --kernel-trace mean of the same timed launches, same command
+                 "rocprof_kernel_ms": (prof.get("kernel_trace") or {}).get("avg_ms"),
+                 "wait_any_frac": prof.get("wait_any_frac"),
+                 "wait_inst_any_frac": prof.get("wait_inst_any_frac")}
     try:
         occupancy = dict(ch.launch_info())
     except AttributeError:  # an A/B library older than fw_chains_launch_info
@@ -438,6 +483,9 @@ def main():
     if prof and prof.get("l2_requests_per_launch") is not None:
         l2 = {"requests_per_launch": prof["l2_requests_per_launch"], "hit": prof.get("l2_hit"),
               "requests_per_attempt": prof["l2_requests_per_launch"] / max(1.0, d["attempts"] / args.steps)}
+    pmc_info = {"key": pmc_key(args.config, args.order, chains, args.inner, args.warmup,
+                               args.steps, lo, resumed),
+                "source": pmc_from, "used": why is None, "reason_null": why}
 
     if rank == 0:
         if args.shard:
@@ -488,10 +536,13 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_null_reason": None if traffic is not None else why,
             },
             "issue_roofline": issue,
             "occupancy": occupancy,
             "l2": l2,
+            "pmc": pmc_info,
+            "identity": identity,
             "kernel_ms": kernel_ms,
             "proposals_per_s": att_all / dt,
             "accepts_per_s": acc_all / dt,

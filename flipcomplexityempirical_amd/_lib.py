@@ -53,6 +53,7 @@ _I32, _I64, _U64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
 SIGNATURES = [
     ("fw_last_error", ctypes.c_char_p, []),
     ("fw_version", _I32, []),
+    ("fw_build_info", ctypes.c_char_p, []),
     ("fw_device_count", _I32, []),
     ("fw_graph_create", ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.c_int, _P]),
     ("fw_graph_destroy", None, [_P]),
@@ -114,19 +115,36 @@ def load(path: str = LIB_PATH):
         except Exception:
             pass
         L = ctypes.CDLL(path)
+        in_tree = os.path.join(_HERE, "libflipwalk.so")
+        is_in_tree = os.path.exists(in_tree) and os.path.samefile(path, in_tree)
+        skipped = []
         for name, res, args in SIGNATURES:
             try:
                 fn = getattr(L, name)
             except AttributeError:
                 # an older build pointed at by FLIPWALK_LIB (A/B runs) may predate an entry
-                # point; the in-tree library must export them all
-                if path == os.path.join(_HERE, "libflipwalk.so"):
+                # point; the in-tree library (by any path or symlink) must export them all
+                if is_in_tree:
                     raise
+                skipped.append(name)
                 continue
             fn.restype = res
             fn.argtypes = args
+        if skipped:
+            import sys
+            print(f"flipwalk: {path} lacks {', '.join(skipped)} (an older build)", file=sys.stderr)
+        L.skipped_symbols = tuple(skipped)
         _lib = L
         return L
+
+
+def build_info() -> str:
+    """fw_build_info() of the loaded library ("src=<hash> flags=<...>"), or a note when the
+    library predates it."""
+    L = load()
+    if "fw_build_info" in getattr(L, "skipped_symbols", ()):
+        return "unknown (library predates fw_build_info)"
+    return L.fw_build_info().decode()
 
 
 def check(rc: int) -> None:

@@ -284,7 +284,7 @@ extern "C" {
 
 const char* fw_last_error(void) { return g_err.c_str(); }
 
-int32_t fw_version(void) { return 0x000600; }
+int32_t fw_version(void) { return 0x000700; }
 
 int32_t fw_device_count(void) {
   int c = 0;
@@ -526,7 +526,8 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     if (!use16 && g->gw == 0 && g->d_ell != nullptr && k <= 31 && lb == 8 && want == 0) {
       const long long gs = round16((int64_t)fw_run_gsum_slots(G) * 2), lds = 160 * 1024;
       const long long wbytes = proposal_mode != FW_PROPOSE_CUTEDGE ? round16(((int64_t)n * 2 + 7) / 8) : 0;
-      const long long l8 = round16(((int64_t)n * 8 + 7) / 8 + 8) + gs + 4 * 128 + wbytes;
+      // the 2-bit LDS proposal weights (p.wb) need 4- or 5-bit labels: only l5 carries them
+      const long long l8 = round16(((int64_t)n * 8 + 7) / 8 + 8) + gs + 4 * 128;
       const long long l5 = round16(((int64_t)n * 5 + 7) / 8 + 8) + gs + 4 * 8 + wbytes;
       if (n > 16384 || std::min(20ll, lds / l5) > std::min(16ll, lds / l8)) lb = 5;
     }
@@ -693,9 +694,11 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
   }
   p.seg_done = c->d_segdone;
-  if ((lb == 3 || lb == 5) && !use16) {  // HBM visit marks of the chain kernel's list search
-    // 4-bit marks of race_search_gscr; 3-bit grids: race_search_b3's byte map
-    p.gscr_words = lb == 3 && g->gw > 0 ? (n + 3) / 4 : (n + 7) / 8;
+  // HBM visit marks of the chain kernel's list search (race_search_gscr: 5-bit labels, and
+  // 3-bit labels off grids); 3-bit grids search with race_search_b3, which keeps its marks
+  // in the labels and looks merge candidates up in its visit list, so they get none
+  if (!use16 && (lb == 5 || (lb == 3 && g->gw == 0))) {
+    p.gscr_words = (n + 7) / 8;  // 4-bit marks, eight per word
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
     if (hipMalloc(&c->d_gscr, gb) != hipSuccess || hipMemset(c->d_gscr, 0, gb) != hipSuccess) {
       fw_chains_destroy(c);

@@ -408,26 +408,6 @@ __device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int
     const uint32_t r0 = __builtin_amdgcn_alignbit(wd[1], wd[0], sh);
     const uint32_t r1 = __builtin_amdgcn_alignbit(wd[2], wd[1], sh);
     const uint32_t r2 = __builtin_amdgcn_alignbit(wd[3], wd[2], sh);
-#ifdef FW_EQ3_SCALAR
-    uint32_t out3 = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const int pos = 3 * j;
-      uint32_t f;
-      if (pos + 3 <= 32)
-        f = (r0 >> pos) & 7u;
-      else if (pos < 32)
-        f = ((r0 >> pos) | (r1 << (32 - pos))) & 7u;
-      else if (pos + 3 <= 64)
-        f = (r1 >> (pos - 32)) & 7u;
-      else if (pos < 64)
-        f = ((r1 >> (pos - 32)) | (r2 << (64 - pos))) & 7u;
-      else
-        f = (r2 >> (pos - 64)) & 7u;
-      out3 |= (f == a ? 1u : 0u) << j;
-    }
-    return out3;
-#else
     const uint32_t pa = a * 0x49249249u;
     const uint32_t y0 = r0 ^ pa, y1 = r1 ^ ((pa << 1) | (a >> 2)), y2 = r2 ^ ((pa << 2) | (a >> 1));
     const uint32_t z0 = y0 | __builtin_amdgcn_alignbit(y1, y0, 1) | __builtin_amdgcn_alignbit(y1, y0, 2);
@@ -441,7 +421,6 @@ __device__ __forceinline__ uint32_t eq_bits32(const LDS uint8_t* lab, int n, int
       return (x ^ (x >> 16)) & 0x000007FFu;
     };
     return compact3(~z0) | (compact3(~z1 >> 1) << 11) | ((compact3(~z2 >> 2) & 0x3FFu) << 22);
-#endif
   }
   uint32_t out = 0;
 #pragma unroll
@@ -686,7 +665,6 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
     uint32_t Qa0 = 0u, Qa1 = 0u, Qb0 = 0u, Qb1 = 0u;  // the previous level, per class
     uint32_t V0 = Fa0 | Fb0, V1 = Fa1 | Fb1;
     int vd = -1;
-#ifndef FW_NO_MID32
     {
       // The race starts on the window's middle 32 columns (vc - 16 .. vc + 15, one VGPR per
       // set: half the work per level) and moves to the 64 columns with its state when a
@@ -729,7 +707,6 @@ __device__ int grid_race_bb2(const LDS uint8_t* lab, int n, int W, int H, int la
       V0 = vv << 16;
       V1 = vv >> 16;
     }
-#endif
     if (vd < 0) for (;;) {
       if (ballot((((Fa0 | Fb0) & E0) | ((Fa1 | Fb1) & E1)) != 0u)) {
         // processed cells (levels < L) and their degrees, counted as the list search counts
@@ -1113,11 +1090,7 @@ struct Ctx {
     } else if constexpr (E16) {
       // lanes 1..16 read v's padded row: its neighbours (a prefix) and so its degree; the
       // rows below are walked up to the largest degree among v and its neighbours
-#ifdef FW_VAR_NODB
-      const int md = g.maxdeg;
-#else
       const int md = rfl(g.dbound[v]);
-#endif
       const int xn = (lane >= 1 && lane <= 16) ? g.ell[(size_t)v * 16 + lane - 1] : -1;
       dv = __popcll(ballot(xn >= 0));
       if (lane > dv) return h;
@@ -1218,11 +1191,7 @@ struct Ctx {
       }
     } else if constexpr (E16) {
       // the group's rows are walked up to its largest degree (C4: 9.7 on average, not 14)
-#ifdef FW_VAR_NODB
-      const int md = g.maxdeg;
-#else
       const int md = rfl(g.dbound[g.n + gi]);
-#endif
       if (x < g.n) weight_row<MODE>(x, md, wx, cd);
     } else {
       if (x < g.n) weight_now<MODE>(x, wx, cd);
@@ -1578,9 +1547,6 @@ struct Ctx {
       return vd;
     }
     // left the window: hand the race to the list search
-#ifdef FW_EXP1
-    return -1;
-#endif
     b3_codes(v, a, m, rs.codes, rs.ambig);
     LDS uint32_t* const stage = reinterpret_cast<LDS uint32_t*>(gsum);
     rs.sv0 = lane < scap ? stage[lane] : 0u;
@@ -2192,10 +2158,7 @@ struct Ctx {
           if (s2.ok) {  // the classes' source indices (CSR order of v's neighbours)
             s2.ra = sx(s2.ra + 1);
             s2.rb = sx(s2.rb + 1);
-#ifndef FW_BB4_ND
-#define FW_BB4_ND 4
-#endif
-            wv = race_bb4<FW_BB4_ND>(v, vr, vc, a, m, s2, bfs_nodes, bfs_deg, rs);
+            wv = race_bb4<4>(v, vr, vc, a, m, s2, bfs_nodes, bfs_deg, rs);
 #ifdef FW_STAMPS
             n_bb4 += 1;
 #endif

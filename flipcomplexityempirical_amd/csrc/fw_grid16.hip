@@ -76,18 +76,11 @@ static_assert(offsetof(fw_chain_stats, yields) == 88 && offsetof(fw_chain_stats,
                   offsetof(fw_chain_stats, cut) == 120 && offsetof(fw_chain_stats, npairs) == 128,
               "fw_chain_stats layout");
 
-// FW_VAR_NOHIST (diagnostic variant only): histogram flushes dropped, to size their write
-// traffic in a PMC pass
-#ifdef FW_VAR_NOHIST
-#define HIST_ADD(ptr, v) ((void)(ptr), (void)(v))
-#else
 #define HIST_ADD(ptr, v) atomicAdd(ptr, v)
-#endif
 
 namespace {
 
 constexpr int ROW = 16;
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr int MAX_NW = 4;          // waves per workgroup
 constexpr uint32_t SCR_BLOCK = 15;  // scratch code of v during a search
 constexpr int LDS_GUARD = 16;       // bytes in front of the first chain slot
@@ -309,9 +302,6 @@ __device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bo
       x = (y | ((y << 1) & ~C0) | ((y >> 1) & ~C6) | (y >> 7) | (y << 7)) & A;
       FLOOD_COUNT;
       if (x == y) break;
-#ifdef FW_VAR_FLOOD3
-      x = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
-#endif
     }
   }
   const uint32_t full = rowbits(ballot(x != 0ull && (x & src) == src), row);
@@ -970,11 +960,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
         const uint32_t w2 = lvl1[wi];  // words past GW (SG) are zero padding
         gs[2 * t] = w2 & 0xFFFFu;
         gs[2 * t + 1] = w2 >> 16;
-#ifdef FW_VAR_DOT2
-        s = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w2), u16x2{1, 1}, s, false);
-#else
         s += gs[2 * t] + gs[2 * t + 1];
-#endif
       }
       const uint32_t incl = row_scan(s);
       const uint32_t rb1 = rowbits(ballot(incl > r), row);

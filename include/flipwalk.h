@@ -152,8 +152,13 @@ const char* fw_last_error(void);
 
 /* Library/ABI version, e.g. 0x000600 for 0.6.0 (0.2: spatial maps; 0.3: bound
  * schedules; 0.4: ring observable, checkpoint/resume; 0.5: sampled geometric waits;
- * 0.6: fw_chains_launch_info). */
+ * 0.6: fw_chains_launch_info; 0.7: fw_build_info). */
 int32_t fw_version(void);
+
+/* Provenance of this build (static string, never NULL): "src=<sha256 of every kernel,
+ * header and ABI source> flags=<compiler flags, including any -D>".  Bench lines and PMC
+ * profiles carry it, so a measurement names the code it measured. */
+const char* fw_build_info(void);
 
 /* Number of visible HIP devices (0 when none; never fails). */
 int32_t fw_device_count(void);

@@ -76,6 +76,24 @@ run_task() {
     prof_c3s8) prof c3s8 "--config c3 --shard 0/8" ;;
     prof_c3s4) prof c3s4 "--config c3 --shard 0/4" ;;
     prof_c3s2) prof c3s2 "--config c3 --shard 0/2" ;;
+    pmc1:*)  # pmc1:TAG:COUNTERS:ARGS:LIB,LIB..  one PMC pass per library (',' for ' ' in
+             # COUNTERS and ARGS), means over the timed dispatches -> OUT/pmc1_TAG.jsonl
+      local rest=${t#pmc1:}; local tag=${rest%%:*}; rest=${rest#*:}
+      local ctrs=${rest%%:*}; rest=${rest#*:}; local args=${rest%%:*}; local libs=${rest#*:}
+      ctrs=${ctrs//,/ }; args=${args//,/ }
+      local k=$(echo " $args " | sed -n 's/.* --steps \([0-9]*\) .*/\1/p')
+      for v in ${libs//,/ }; do
+        local lib=${v%%@*} envs=""
+        [ "$lib" != "$v" ] && envs=${v#*@}
+        rm -rf $O/pmc1_${tag}_$lib
+        env $envs FLIPWALK_LIB=$PWD/ab/lib_$lib.so timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/pmc1_${tag}_$lib -o run --output-format csv -- python3 bench.py $args --no-cpu-baseline --check-chains 0 > $O/pmc1_${tag}_$lib.log 2>&1 || { echo "pmc $v failed"; tail -5 $O/pmc1_${tag}_$lib.log; return 1; }
+        python3 scripts/pmc_one.py $O/pmc1_${tag}_$lib ${k:-1} $v | tee -a $O/pmc1_$tag.jsonl
+      done ;;
+    stamps:*)  # stamps:CONFIG:CHAINS[:ENV=VAL] (grid kernel phases, 2 warm launches)
+      local r=${t#stamps:}; local cfg=${r%%:*}; r=${r#*:}; local nch=${r%%:*}; local ev=""
+      [ "$r" != "$nch" ] && ev=${r#*:}
+      env $ev timeout -k 10 300 python -u scripts/stamps.py $cfg $nch 2 > $O/stamps_${cfg}_${nch}${ev:+_$ev}.txt 2>&1 || { tail -5 $O/stamps_${cfg}_${nch}${ev:+_$ev}.txt; return 1; }
+      grep -v amdgpu.ids $O/stamps_${cfg}_${nch}${ev:+_$ev}.txt ;;
     stamps_c5)
       timeout -k 10 300 python -u scripts/stamps.py c5 8192 1 $CK5 > $O/stamps_c5_100k.txt 2>&1 || { tail -5 $O/stamps_c5_100k.txt; return 1; }
       grep -v amdgpu.ids $O/stamps_c5_100k.txt ;;

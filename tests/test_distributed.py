@@ -232,3 +232,31 @@ def test_bench_under_torchrun_two_ranks(tmp_path, gpu_lib):
     a, b = np.load(h2), np.load(h1)
     for key in ("hist_cut", "hist_b", "final"):
         assert np.array_equal(a[key], b[key]), key
+
+
+@pytest.mark.gpu
+def test_bench_rccl_branch_under_torchrun(tmp_path, gpu_lib):
+    """bench.py's RCCL path itself: launched by torch.distributed.run (one rank, a fresh
+    child process), it opens the "nccl" process group and runs its device-tensor
+    all-reduces (max-over-ranks time, step / attempt sums, the checker totals, the
+    histogram merge) over RCCL.  Every checked chain equals the oracle and every yield
+    lands in exactly one bin of each merged histogram."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
+                        str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "1",
+                        "--backend", "nccl", "--config", "c3", "--chains", "8192", "--steps", "2",
+                        "--warmup", "1", "--inner", "300", "--no-cpu-baseline",
+                        "--check-chains", "4"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    pc = line["parity_check"]
+    assert pc["ranks"] == 1 and pc["equal"] == pc["chains"] >= 4, pc
+    assert pc["hist_yields_equal"]
+    assert line["hist_yields"] == 8192 * (3 * 300 + 1)
+    assert "RCCL" in line["config"]["parallelism"], line["config"]["parallelism"]

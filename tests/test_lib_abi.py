@@ -31,8 +31,25 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_version_and_device_count_without_gpu():
     L = _lib.load()
-    assert L.fw_version() == 0x000600
+    assert L.fw_version() == 0x000700
     assert L.fw_device_count() >= 0
+
+
+def test_build_info_names_sources_and_flags():
+    """fw_build_info: a hash over the kernel / header / ABI sources and the compile flags
+    (bench lines and PMC profiles carry it); a rebuilt in-tree library hashes the
+    sources as they are now."""
+    import hashlib
+    info = _lib.build_info()
+    m = re.match(r"src=([0-9a-f]{16}) flags=(.*)$", info)
+    assert m, info
+    assert "--offload-arch=gfx950" in m.group(2)
+    csrc = os.path.join(ROOT, "flipcomplexityempirical_amd", "csrc")
+    blob = b"".join(open(os.path.join(csrc, f), "rb").read() for f in
+                    ("fw_api.hip", "fw_kernels.hip", "fw_grid16.hip", "fw_internal.h",
+                     "fw_device.h", "fw_math.h"))
+    blob += open(os.path.join(ROOT, "include", "flipwalk.h"), "rb").read()
+    assert m.group(1) == hashlib.sha256(blob).hexdigest()[:16], "library older than its sources"
 
 
 def _csr(adj):
