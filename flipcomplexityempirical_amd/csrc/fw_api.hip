@@ -698,7 +698,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   // 3-bit labels off grids); 3-bit grids search with race_search_b3, which keeps its marks
   // in the labels and looks merge candidates up in its visit list, so they get none
   if (!use16 && (lb == 5 || (lb == 3 && g->gw == 0))) {
-    p.gscr_words = (n + 7) / 8;  // 4-bit marks, eight per word
+    p.gscr_words = n;  // one 32-bit mark per node (race_search_gscr)
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
     if (hipMalloc(&c->d_gscr, gb) != hipSuccess || hipMemset(c->d_gscr, 0, gb) != hipSuccess) {
       fw_chains_destroy(c);

@@ -861,8 +861,8 @@ struct Ctx {
   LDS uint32_t* wts;   // select<.., WB>: 2-bit per-node weights (node x at bits 2x), saturated at 3
   LDS uint32_t* list;  // LDS part of the search list
   GLB uint32_t* spill; // HBM part (this workgroup's slice)
-  GLB uint32_t* gscr;  // LB == 3, 5: this workgroup's 4-bit visit marks in HBM (all zero
-                       // between searches; such labels cannot hold the search codes)
+  GLB uint32_t* gscr;  // race_search_gscr: this workgroup's 32-bit visit mark per node in
+                       // HBM (all zero between searches; 5-bit labels cannot hold the codes)
   int32_t qcap, k;
   int32_t scap;  // race_search_b3: next-level entries staged over the group sums (<= 128)
   int lane;
@@ -1208,48 +1208,45 @@ struct Ctx {
   }
 
   // -------------------------------------------------------------- contiguity
-  // -- 4-bit visit marks in HBM (LB == 3).  Agent-scope atomics and loads: the marks are
-  // read back within the same search, so no access may be served by a stale L1 line.
-  __device__ __forceinline__ uint32_t gs_get(int x) const {
-    return (__hip_atomic_load(gscr + (x >> 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
-            ((x & 7) << 2)) & 15u;
+  // -- visit marks in HBM (LB == 5; 3-bit labels off grids): one 32-bit word per node in
+  // this workgroup's slice of gscr, 0 = unvisited, 1 + source index, 15 = v.  A claim is
+  // ONE compare-and-swap that returns the mark it found (the class of an already visited
+  // node): no separate load and no retry loop, as 4-bit marks sharing a word needed
+  // (Hilbert-numbered neighbours share words, so their claims collided).  Agent-scope
+  // atomics: they execute in the L2, and the marks are read back within the same search.
+  __device__ __forceinline__ void gm_set(int x, uint32_t code) const {
+    __hip_atomic_store(gscr + x, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __device__ __forceinline__ void gs_xor(int x, uint32_t d) const {
-    __hip_atomic_fetch_xor(gscr + (x >> 3), d << ((x & 7) << 2), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __device__ __forceinline__ void gs_clear(int x) const {
-    __hip_atomic_fetch_and(gscr + (x >> 3), ~(15u << ((x & 7) << 2)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // claim mark x: 0 -> code if still unvisited; returns the mark found (0 on success)
-  __device__ __forceinline__ uint32_t gs_claim(int x, uint32_t code) const {
-    GLB uint32_t* w = gscr + (x >> 3);
-    const int sh = (x & 7) << 2;
-    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      const uint32_t cur = (old >> sh) & 15u;
-      if (cur != 0u) return cur;
-      if (__hip_atomic_compare_exchange_strong(w, &old, old | (code << sh), __ATOMIC_RELAXED,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        return 0u;
-    }
+  __device__ __forceinline__ uint32_t gm_claim(int x, uint32_t code) const {
+    uint32_t old = 0u;
+    __hip_atomic_compare_exchange_strong(gscr + x, &old, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return old;  // 0: claimed (the CAS stored code); else the mark found
   }
 
-  // The race search with the visit marks in gscr (1 + source index, 15 = v) instead of in
-  // the labels (3- and 5-bit labels cannot hold the codes): the same levels, pushes, merges
-  // and counters as race_search (and as the grid kernel's grid_race).
+  // The race search with the visit marks in gscr instead of in the labels (5-bit labels
+  // cannot hold the codes): the same levels, pushes, merges and counters as race_search
+  // (and as the grid kernel's grid_race).  A level's nodes are processed four at a time,
+  // sixteen lanes per node, lane j of a node's group taking its padded row's entry j: one
+  // round of dependent memory trips (row entry, label, claim) serves every neighbour of four
+  // nodes, where a lane per node walked its row entry by entry, two L2 round trips per entry
+  // (C4: ~50,000 cycles per run, the kernel's largest cost).  The order in which a level's
+  // claims are made changes no level, verdict or counter (the merges they produce do not
+  // depend on it: grid_race_bb).  A list entry carries its node's source index (node |
+  // index << 28), so the node's mark is never read back.
   __device__ bool race_search_gscr(int v, uint32_t a, int m, int src, uint64_t cls,
                                    uint64_t& bfs_nodes, uint64_t& bfs_deg) {
-    if (lane == 0) gs_xor(v, 15u);
+    constexpr uint32_t XM = (1u << 28) - 1u;
+    if (lane == 0) gm_set(v, 15u);
     if (lane < m) {
-      gs_xor(src, 1u + (uint32_t)lane);
-      list_put(lane, (uint32_t)src);
+      gm_set(src, 1u + (uint32_t)lane);
+      list_put(lane, (uint32_t)src | ((uint32_t)lane << 28));
     }
     __threadfence_block();
     int nl = m, lb = 0, le = m;
     uint32_t my_deg = 0;
     int verdict = -1;
+    const int j = lane & 15;
     for (;;) {
       uint64_t rep = ballot(lane < m && (__ffsll((unsigned long long)cls) - 1) == lane);
       if (__popcll(rep) == 1) {
@@ -1258,41 +1255,29 @@ struct Ctx {
       }
       uint64_t pushed_src = 0;
       for (int base = lb; base < le; base += WAVE) {
-        const int idx = base + lane;
-        const bool act = idx < le;
-        const int x = act ? (int)list_get(idx) : 0;
-        const uint32_t o = act ? gs_get(x) - 1u : 0u;
-        int xr = 0, xc = 0;
-        int dmax = 0;
-        int r16[16];
-        if constexpr (E16) {
-          if (act) {
-            row16(x, r16);
-#pragma unroll
-            for (int j = 0; j < 16; ++j) dmax += r16[j] >= 0 ? 1 : 0;
-            my_deg += (uint32_t)dmax;
+        const int nb = min(WAVE, le - base);
+        bfs_nodes += (uint64_t)nb;
+        for (int f0 = 0; f0 < nb; f0 += 4) {
+          const int f = f0 + (lane >> 4);
+          const bool fa = f < nb;
+          // the node's entry (16 lanes read the same word), then its row entry j
+          const uint32_t e = fa ? list_get(base + f) : 0u;
+          const int x = (int)(e & XM);
+          const uint32_t o = e >> 28;
+          int y = -1;
+          if constexpr (E16) {
+            y = fa ? g.ell[(size_t)x * 16 + j] : -1;
+          } else {
+            int xr = 0, xc = 0;
+            if constexpr (GRID) divmod(x, xr, xc);
+            // CSR rows of degree <= 16 (one group per node); grids: slots 0..3
+            y = fa && (!GRID || j < 4) ? nbr(x, j, xr, xc) : -1;
           }
-        } else if (act) {
-          if constexpr (GRID) divmod(x, xr, xc);
-          dmax = GRID ? 4 : g.rowptr[x + 1] - g.rowptr[x];
-          my_deg += (uint32_t)degree(x, xr, xc);
-        }
-        bfs_nodes += (uint64_t)__popcll(ballot(act));
-        int jmax = 4;
-        if constexpr (!GRID) {
-          jmax = (int)wave_max32((uint32_t)dmax);
-        }
-        for (int j = 0; j < (E16 ? 16 : 64); ++j) {  // r16[j]: uniform j
-          if (j >= jmax) break;  // uniform
-          int y;
-          if constexpr (E16)
-            y = (act && j < dmax) ? r16[j] : -1;
-          else
-            y = (act && j < dmax) ? nbr(x, j, xr, xc) : -1;
+          my_deg += y >= 0 ? 1u : 0u;
           bool push = false, req = false;
           uint32_t other = 0;
           if (y >= 0 && L(y) == a) {
-            const uint32_t got = gs_claim(y, 1u + o);
+            const uint32_t got = gm_claim(y, 1u + o);
             if (got == 0u) {
               push = true;
             } else if (got - 1u < (uint32_t)m) {  // v (15) is never a class
@@ -1301,7 +1286,7 @@ struct Ctx {
             }
           }
           const uint64_t pm = ballot(push);
-          if (push) list_put(nl + (int)mbcnt(pm), (uint32_t)y);
+          if (push) list_put(nl + (int)mbcnt(pm), (uint32_t)y | (o << 28));
           nl += __popcll(pm);
           if (pm) {
             for (int si = 0; si < m; ++si)
@@ -1338,9 +1323,9 @@ struct Ctx {
     bfs_deg += wave_sum(my_deg);
     for (int base = 0; base < nl; base += WAVE) {  // clear the visit marks
       const int idx = base + lane;
-      if (idx < nl) gs_clear((int)list_get(idx));
+      if (idx < nl) gm_set((int)(list_get(idx) & XM), 0u);
     }
-    if (lane == 0) gs_clear(v);
+    if (lane == 0) gm_set(v, 0u);
     __threadfence_block();
     return verdict == 1;
   }
@@ -1451,11 +1436,15 @@ struct Ctx {
     const uint32_t fdeg0 = (uint32_t)((re > 0) + (re < H - 1) + 2);
     const uint32_t fdeg1 = (uint32_t)((re + 1 > 0) + (re + 1 < H - 1) + 2);
     const int w0 = -C0, w1 = W - 1 - C0;  // window positions of grid columns 0 and W - 1
+    // bit `pos` (wave-uniform) of a row held as ND dwords.  The dword is picked by masks,
+    // not by a select over an array: LLVM turned that select into an indexed load of a
+    // stack copy of the array (a scratch store and load per call, C5's only non-spill
+    // scratch traffic)
     auto wbit = [](const uint32_t (&f)[ND], int pos) -> uint32_t {
-      uint32_t dd = f[0];
+      const int sel = pos >> 5;
+      uint32_t dd = 0u;
 #pragma unroll
-      for (int d = 1; d < ND; ++d)
-        if (pos >= 32 * d) dd = f[d];
+      for (int d = 0; d < ND; ++d) dd |= f[d] & (0u - (uint32_t)(sel == d));
       return (dd >> (pos & 31)) & 1u;
     };
     // The processed cells are counted once, after the loop: they are the frontier handed

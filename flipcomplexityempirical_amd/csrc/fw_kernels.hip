@@ -268,6 +268,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       bool valid = false;
       for (;;) {
         CSTAMP(-1);
+        // 3-bit grids (C5): the lane id made opaque each attempt, so the lane-derived
+        // constants are recomputed in the loop instead of hoisted to the kernel entry and
+        // spilled (31 -> 6 VGPRs of scratch, C5 +2.2%; the other instantiations, which do
+        // not spill, lose 0.5-3.5% to the recomputation: profiles/r05/opaque_lane/)
+        if constexpr (LB == 3 && GRID) asm volatile("" : "+v"(C.lane));
         if (retries >= p.max_retries || npairs == 0) {
           stuck = 1;
           break;
