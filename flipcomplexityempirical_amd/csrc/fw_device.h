@@ -1257,14 +1257,13 @@ struct Ctx {
       for (int base = lb; base < le; base += WAVE) {
         const int nb = min(WAVE, le - base);
         bfs_nodes += (uint64_t)nb;
-        for (int f0 = 0; f0 < nb; f0 += 4) {
+        // the node's entry (its group's 16 lanes read the same word), then its row entry j;
+        // the next four nodes' are fetched while this step's claims are made
+        auto fetch = [&](int f0, uint32_t& e, int& y) {
           const int f = f0 + (lane >> 4);
           const bool fa = f < nb;
-          // the node's entry (16 lanes read the same word), then its row entry j
-          const uint32_t e = fa ? list_get(base + f) : 0u;
+          e = fa ? list_get(base + f) : 0u;
           const int x = (int)(e & XM);
-          const uint32_t o = e >> 28;
-          int y = -1;
           if constexpr (E16) {
             y = fa ? g.ell[(size_t)x * 16 + j] : -1;
           } else {
@@ -1273,6 +1272,15 @@ struct Ctx {
             // CSR rows of degree <= 16 (one group per node); grids: slots 0..3
             y = fa && (!GRID || j < 4) ? nbr(x, j, xr, xc) : -1;
           }
+        };
+        uint32_t e_n;
+        int y_n;
+        fetch(0, e_n, y_n);
+        for (int f0 = 0; f0 < nb; f0 += 4) {
+          const uint32_t e = e_n;
+          const int y = y_n;
+          if (f0 + 4 < nb) fetch(f0 + 4, e_n, y_n);
+          const uint32_t o = e >> 28;
           my_deg += y >= 0 ? 1u : 0u;
           bool push = false, req = false;
           uint32_t other = 0;
