@@ -448,7 +448,7 @@ def main():
     identity = {
         "config": args.config, "order": args.order, "grid": args.grid, "k": k,
         "proposal": proposal, "base": base_desc, "percent": percent, "seed": args.seed,
-        "chains": chains, "chain_id0": lo, "world": world, "inner": args.inner,
+        "chains": chains, "chain_id0": lo, "inner": args.inner,
         "warmup": args.warmup, "steps": args.steps, "resumed_steps": resumed,
         "maps": bool(args.maps), "flipwalk_env": flipwalk_env(), "build": build_info(),
     }

@@ -68,6 +68,11 @@ run_task() {
       local lib=${t#prof_c5:}
       FLIPWALK_LIB=$PWD/ab/lib_$lib.so prof c5steady_$lib "--config c5 --shard 0/8 --resume $CK5 --check-chains 0" "--steps 5 --warmup 0 --inner 1000 --no-cpu-baseline --config c5 --shard 0/8 --resume $CK5 --check-chains 0" ;;
     prof_c5fresh) prof c5fresh "--config c5 --shard 0/8" ;;
+    profile:*)  # profile:TAG:BENCH_ARGS (',' for ' '): profile.sh passes of exactly that protocol
+      local r=${t#profile:}; local tag=${r%%:*}; local a=${r#*:}; a=${a//,/ }
+      BENCH_ARGS="$a --no-cpu-baseline --check-chains 0" timeout -k 10 1100 bash scripts/profile.sh $tag > "$O/prof_$tag.log" 2>&1 \
+        || { echo "profile $tag failed"; tail -20 "$O/prof_$tag.log"; return 1; }
+      grep -E "traffic ->|timed=" "$O/prof_$tag.log" ;;
     prof_c4) prof c4 "--config c4" ;;
     prof_c4r) prof c4r "--config c4 --order random" ;;
     prof_frank) prof frank "--config frank" ;;

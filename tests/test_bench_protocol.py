@@ -7,7 +7,7 @@ import bench
 def _ident(**kw):
     d = {"config": "c3", "order": None, "grid": None, "k": 4, "proposal": "pairs",
          "base": "base mu", "percent": 0.05, "seed": 0, "chains": 65536, "chain_id0": 0,
-         "world": 1, "inner": 1000, "warmup": 5, "steps": 20, "resumed_steps": 0, "maps": False,
+         "inner": 1000, "warmup": 5, "steps": 20, "resumed_steps": 0, "maps": False,
          "flipwalk_env": {}, "build": "src=0123456789abcdef flags=-O3"}
     d.update(kw)
     return d
