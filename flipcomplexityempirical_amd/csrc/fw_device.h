@@ -1209,7 +1209,7 @@ struct Ctx {
 
   // -------------------------------------------------------------- contiguity
   // -- visit marks in HBM (LB == 5; 3-bit labels off grids): one 32-bit word per node in
-  // this workgroup's slice of gscr, 0 = unvisited, 1 + source index, 15 = v.  A claim is
+  // this workgroup's slice of gscr, 0 = unvisited, 1 + source index, ~0 = v.  A claim is
   // ONE compare-and-swap that returns the mark it found (the class of an already visited
   // node): no separate load and no retry loop, as 4-bit marks sharing a word needed
   // (Hilbert-numbered neighbours share words, so their claims collided).  Agent-scope
@@ -1237,7 +1237,7 @@ struct Ctx {
   __device__ bool race_search_gscr(int v, uint32_t a, int m, int src, uint64_t cls,
                                    uint64_t& bfs_nodes, uint64_t& bfs_deg) {
     constexpr uint32_t XM = (1u << 28) - 1u;
-    if (lane == 0) gm_set(v, 15u);
+    if (lane == 0) gm_set(v, ~0u);  // v: never a class (any m, up to the row's 16 sources)
     if (lane < m) {
       gm_set(src, 1u + (uint32_t)lane);
       list_put(lane, (uint32_t)src | ((uint32_t)lane << 28));
@@ -1288,7 +1288,7 @@ struct Ctx {
             const uint32_t got = gm_claim(y, 1u + o);
             if (got == 0u) {
               push = true;
-            } else if (got - 1u < (uint32_t)m) {  // v (15) is never a class
+            } else if (got - 1u < (uint32_t)m) {  // v (~0) is never a class
               req = true;
               other = got - 1u;
             }
