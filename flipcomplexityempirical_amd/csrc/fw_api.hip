@@ -724,6 +724,11 @@ static int launch_slices(const fw_chains* c, int64_t steps) {
   const long long s_max = std::max<long long>(1, std::min<long long>(8, 0x7FFFFFFFll / std::max(nq, 1ll)));
   if (force >= 1) return (int)std::min<long long>({(long long)force, std::max<int64_t>(steps, 1), s_max});
   if (nq <= W || steps < 64) return 1;
+  // chains of a small state (C2's 40x40 grid: 400 B of labels) restart a slice for almost
+  // nothing, and more, shorter units even out the units' unequal durations at the end of the
+  // launch: the most slices (C2 at S = 3 / 6 / 8: 1.314 / 1.340 / 1.347 x 10^9; C3 at 6 and
+  // C4 at 8 lose 0.2% / 2.8%: profiles/r05/slices/)
+  if (c->p.lab_bytes <= 1024) return (int)std::min<long long>(s_max, steps / 64);
   int best = 1;
   double best_t = 1e300;
   for (int S = 1; S <= s_max; ++S) {
