@@ -91,3 +91,16 @@ slot = (hw & 0xF).astype(np.int64)
 for s_ in np.unique(slot[early]):
     m = early & (slot == s_)
     print(f"  wave slot {s_}: n={m.sum():5d} duration mean {dur[m].mean():.1f}")
+
+# per XCD (XCC_ID, the high word): a slower die shows as a shifted duration distribution
+xcc = ((hw >> 32) & 0xF).astype(np.int64)
+for x_ in np.unique(xcc):
+    m = xcc == x_
+    print(f"  XCD {x_}: n={m.sum():5d} duration mean {dur[m].mean():.1f} p10 {np.percentile(dur[m], 10):.1f} "
+          f"p90 {np.percentile(dur[m], 90):.1f} max {dur[m].max():.1f}")
+# per quad: the quad's own chains (attempts this launch) vs its duration
+if len(t) == nq:
+    se = ((hw >> 13) & 7).astype(np.int64)
+    for s_ in np.unique(se):
+        m = se == s_
+        print(f"  SE {s_}: n={m.sum():5d} duration mean {dur[m].mean():.1f}")
