@@ -12,13 +12,13 @@ mu = 2.63815853 (grid_chain_sec11.py:33,171-179).  ``--scaling weak`` gives ever
 
 A bench "step" is one kernel launch that advances every chain by --inner counted flip
 steps (valid proposals, MarkovChain counter increments); value = counted flip steps of
-all chains on all ranks / max-over-ranks wall time of the K timed launches.  --inner is
-5,000 (rounds 1-5: 1,000): a launch lasts as long as its slowest chain, and where every
-chain has its own wave slot (an 8-GPU job's 8,192-chain shard, C2) that wait was 10-20% of
-a 1,000-step launch (profiles/r05/unit_times/, launch_length/); the reference runs its
-10^5 steps per chain as one loop (grid_chain_sec11.py:342), which the library runs as one
-launch.  The steady state of SURVEY.md §8d (10^4 warm-up + 10^5 timed steps per chain) is
---warmup 2 --steps 20.
+all chains on all ranks / max-over-ranks wall time of the K timed launches.  A launch
+lasts as long as its slowest chain: where every chain has its own wave slot (an 8-GPU
+job's 8,192-chain shard, C2) that wait is 10-20% of a 1,000-step launch and shrinks with
+longer launches (profiles/r05/unit_times/, launch_length/).  The reference runs its 10^5
+steps per chain as one loop (grid_chain_sec11.py:342), which the library runs as one
+launch; SURVEY.md §8d's steady state (10^4 warm-up + 10^5 timed steps per chain) is
+measured as --inner 5000 --warmup 2 --steps 20.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -278,7 +278,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inner", type=int, default=5000,
+    ap.add_argument("--inner", type=int, default=1000,
                     help="flip steps per chain per launch (see the module docstring)")
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5", "frank"],
                     help="workload (flipcomplexityempirical_amd/workloads.py); the driver's line "

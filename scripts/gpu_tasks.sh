@@ -14,8 +14,8 @@
 #   prof_c4 / prof_c3 / prof_c2 / prof_c3s8
 #                         kernel trace + PMC of C4 / C3 / C2 / the 8,192-chain C3 shard
 #   stamps_c5 / stamps_c4 per-phase clocks (stamps build) at the C5 checkpoint / C4
-#   steady                SURVEY 8d's steady state (10^4 + 10^5 steps: --warmup 2 --steps 20
-#                         at 5,000 steps per launch) on every workload -> OUT/steady.jsonl
+#   steady                SURVEY 8d's steady state (10^4 + 10^5 steps: --inner 5000
+#                         --warmup 2 --steps 20) on every workload -> OUT/steady.jsonl
 #   ab:TAG:ARGS:LIB,LIB.. interleaved A/B of ab/lib_<LIB>.so builds (3 rounds) -> OUT/ab_TAG.jsonl
 #                         (LIB@VAR=VALUE: with one environment setting)
 #   multi                 bench.py under torch.distributed.run, 2 gloo ranks on device 0
@@ -61,7 +61,7 @@ run_task() {
       tail -1 $O/one.json >> $O/bench.jsonl
       line $O/one.json "$a" ;;
     ck_c5)
-      timeout -k 10 300 python -u bench.py --config c5 --shard 0/8 --inner 1000 --warmup 0 --steps 100 --check-chains 0 --no-cpu-baseline --save-checkpoint $CK5 > $O/ck_c5.json 2> $O/ck_c5.err || { tail -5 $O/ck_c5.err; return 1; }
+      timeout -k 10 300 python -u bench.py --config c5 --shard 0/8 --warmup 0 --steps 100 --check-chains 0 --no-cpu-baseline --save-checkpoint $CK5 > $O/ck_c5.json 2> $O/ck_c5.err || { tail -5 $O/ck_c5.err; return 1; }
       line $O/ck_c5.json ck_c5 ;;
     prof_c5)
       prof c5steady "--config c5 --shard 0/8 --resume $CK5 --check-chains 0" "--steps 5 --warmup 0 --inner 1000 --no-cpu-baseline --config c5 --shard 0/8 --resume $CK5 --check-chains 0" ;;
@@ -111,7 +111,7 @@ run_task() {
       grep -v amdgpu.ids $O/stamps_c4.txt ;;
     steady)
       for a in "--config c3" "--config c2" "--config c4" "--config c5 --shard 0/8" "--config frank" "--config c3 --shard 0/8"; do
-        timeout -k 10 300 python -u bench.py $a --warmup 2 --steps 20 --no-cpu-baseline --check-chains 2 > $O/one.json 2> $O/one.err || { echo "$a failed"; tail -5 $O/one.err; return 1; }
+        timeout -k 10 300 python -u bench.py $a --inner 5000 --warmup 2 --steps 20 --no-cpu-baseline --check-chains 2 > $O/one.json 2> $O/one.err || { echo "$a failed"; tail -5 $O/one.err; return 1; }
         tail -1 $O/one.json >> $O/steady.jsonl
         line $O/one.json "$a"
       done ;;
@@ -129,7 +129,7 @@ run_task() {
         done
       done ;;
     shards_c5)  # the 8-GPU C5 job emulated shard by shard at the steady-state protocol
-      timeout -k 10 900 bash scripts/shards.sh 8 "--config c5 --steps 20 --warmup 2 --check-chains 2" c5 > $O/shards_c5.log 2>&1 || { tail -5 $O/shards_c5.log; return 1; }
+      timeout -k 10 900 bash scripts/shards.sh 8 "--config c5 --inner 5000 --steps 20 --warmup 2 --check-chains 2" c5 > $O/shards_c5.log 2>&1 || { tail -5 $O/shards_c5.log; return 1; }
       tail -10 $O/shards_c5.log ;;
     shards_c3)  # the 8-GPU C3 job emulated shard by shard on the driver protocol
       timeout -k 10 600 bash scripts/shards.sh 8 "--config c3 --steps 20 --warmup 5 --check-chains 2" c3 > $O/shards_c3.log 2>&1 || { tail -5 $O/shards_c3.log; return 1; }
