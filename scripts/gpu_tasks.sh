@@ -134,6 +134,9 @@ run_task() {
     shards_c3)  # the 8-GPU C3 job emulated shard by shard on the driver protocol
       timeout -k 10 600 bash scripts/shards.sh 8 "--config c3 --steps 20 --warmup 5 --check-chains 2" c3 > $O/shards_c3.log 2>&1 || { tail -5 $O/shards_c3.log; return 1; }
       tail -10 $O/shards_c3.log ;;
+    shards_c3s)  # the 8-GPU C3 job emulated shard by shard at the steady state
+      timeout -k 10 900 bash scripts/shards.sh 8 "--config c3 --inner 5000 --steps 20 --warmup 2 --check-chains 2" c3steady > $O/shards_c3steady.log 2>&1 || { tail -5 $O/shards_c3steady.log; return 1; }
+      tail -10 $O/shards_c3steady.log ;;
     multi)
       timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --config c3 --chains 8192 --steps 2 --warmup 1 --backend gloo --same-device --no-cpu-baseline --check-chains 4 > $O/multi.json 2> $O/multi.err || { tail -20 $O/multi.err; return 1; }
       tail -1 $O/multi.json ;;
