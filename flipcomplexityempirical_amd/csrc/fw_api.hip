@@ -688,6 +688,7 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
   p.spill = c->d_spill;
   p.next_chain = c->d_next;
   p.slices = 1;
+  p.prio_shift = 5;
   // one per chain: enough for every kernel's work units (quads, pairs or chains)
   if (hipMalloc(&c->d_segdone, sizeof(int32_t) * (size_t)n_chains) != hipSuccess) {
     fw_chains_destroy(c);
@@ -742,6 +743,16 @@ static int launch_slices(const fw_chains* c, int64_t steps) {
   return best;
 }
 
+// The grid kernel's wave-priority levels (fw_grid16_kernel): eighths of a unit's steps when
+// every unit has a wave slot of its own (the 8,192-chain shard: +1.4% over 32nds), quarters
+// when waves take several units (C2 +1.2%, C3 +0.3%; 16ths and 128ths lose 0.5% / 1.6% on
+// C3: profiles/r05/prio_levels/)
+static int launch_prio_shift(const fw_chains* c) {
+  const long long nu = slice_units(c) * (long long)c->p.slices;
+  const long long W = (long long)c->grid * (c->p.use16 ? fw_grid16_launch_nw(c->p) : 1);
+  return nu <= W ? 3 : 2;
+}
+
 int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
   if (!c || steps < 0 || max_retries <= 0) return fail(FW_EINVAL, "fw_chains_run: bad arguments");
   HIPCHK(hipSetDevice(c->g->device));
@@ -768,6 +779,7 @@ int fw_chains_run_async(fw_chains* c, int64_t steps, int32_t max_retries) {
     c->p.steps = s;
     c->p.gcache_ok = c->gcache_ok ? 1 : 0;
     c->p.slices = !c->p.trace ? launch_slices(c, s) : 1;
+    c->p.prio_shift = launch_prio_shift(c);
     if (c->p.slices > 1)
       HIPCHK(hipMemsetAsync(c->d_segdone, 0, sizeof(int32_t) * (size_t)slice_units(c), c->stream));
     HIPCHK(hipMemsetAsync(c->d_next, 0, sizeof(int32_t), c->stream));

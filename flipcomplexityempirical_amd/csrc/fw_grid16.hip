@@ -880,10 +880,11 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
     // older one: at equal priority the younger waves of a SIMD get the leftover slots and
     // finish their units ~25% later (8,192 chains, 2 waves per SIMD: 2.38 vs 3.01 ms,
     // scripts/unit_times.py), and with no more units to take the launch waits for them.
-    // Priority 3 - (level mod 4), the level counting 32nds of the unit's steps done by
-    // row 0, hands the issue slots to the wave one level behind (except across a wrap),
-    // which keeps a SIMD's waves within about one level of each other to the end.
-    const uint32_t pstep = ustep >= 64u ? ustep >> 5 : 2u;
+    // Priority 3 - (level mod 4), the level counting 2^-prio_shift of the unit's steps done
+    // by row 0 (launch_prio_shift: 8ths or quarters), hands the issue slots to the wave one
+    // level behind (except across a wrap), which keeps a SIMD's waves close to the end.
+    const uint32_t psh = (uint32_t)p.prio_shift;
+    const uint32_t pstep = ustep >= (2u << psh) ? ustep >> psh : 2u;
     uint32_t pnext = pstep, plev = 0;
     __builtin_amdgcn_s_setprio(3);
     for (;;) {

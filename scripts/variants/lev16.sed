@@ -1,0 +1,2 @@
+# diagnostic variant: the grid kernel's wave-priority levels in 16ths of a unit's steps
+s|const uint32_t pstep = ustep >= 64u ? ustep >> 5 : 2u;|const uint32_t pstep = ustep >= 32u ? ustep >> 4 : 2u;|
