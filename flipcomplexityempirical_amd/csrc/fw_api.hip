@@ -743,10 +743,10 @@ static int launch_slices(const fw_chains* c, int64_t steps) {
   return best;
 }
 
-// The grid kernel's wave-priority levels (fw_grid16_kernel): eighths of a unit's steps when
-// every unit has a wave slot of its own (the 8,192-chain shard: +1.4% over 32nds), quarters
-// when waves take several units (C2 +1.2%, C3 +0.3%; 16ths and 128ths lose 0.5% / 1.6% on
-// C3: profiles/r05/prio_levels/)
+// The kernels' wave-priority levels (fw_grid16_kernel, fw_run_kernel): eighths of a unit's
+// steps when every unit has a wave slot of its own (the 8,192-chain shard: +1.4% over 32nds),
+// quarters when waves take several units (C2 +1.2%, C3 +0.3%, C4 / C5 / Frankengraph
+// +0.4-0.6%; 16ths and 128ths lose 0.5% / 1.6% on C3: profiles/r05/prio_levels/)
 static int launch_prio_shift(const fw_chains* c) {
   const long long nu = slice_units(c) * (long long)c->p.slices;
   const long long W = (long long)c->grid * (c->p.use16 ? fw_grid16_launch_nw(c->p) : 1);

@@ -94,7 +94,7 @@ struct FwRunParams {
   // quad's finished slices (zeroed before a launch with slices > 1)
   int32_t slices;
   int32_t* seg_done;
-  // grid kernel: a wave's priority level counts 2^-prio_shift of its unit's steps
+  // both kernels: a wave's priority level counts 2^-prio_shift of its unit's steps
   int32_t prio_shift;
   // spatial observables (nullptr: off).  Per chain c: acc [E] (int64: sum of -t when an
   // edge becomes cut and +t when it becomes uncut, so cut_times = acc + [cut now] * Y),

@@ -246,7 +246,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // wave priority 3 - (level mod 4), the level counting 32nds of the unit's steps: the
     // SIMD's VALU goes to the wave one level behind instead of the oldest (see
     // fw_grid16_kernel), so the waves of the last residency round finish together
-    const int64_t pstep = ustep >= 64 ? ustep >> 5 : 2;
+    const int psh = p.prio_shift;  // launch_prio_shift (C4 / C5 / Frankengraph +0.4-0.6%)
+    const int64_t pstep = ustep >= (int64_t(2) << psh) ? ustep >> psh : 2;
     int64_t pnext = pstep;
     uint32_t plev = 0;
     __builtin_amdgcn_s_setprio(3);
