@@ -886,7 +886,11 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
     const uint32_t psh = (uint32_t)p.prio_shift;
     const uint32_t pstep = ustep >= (2u << psh) ? ustep >> psh : 2u;
     uint32_t pnext = pstep, plev = 0;
-    __builtin_amdgcn_s_setprio(3);
+    // one unit per wave slot (psh == 3): the older wave of a SIMD (even slot) wins priority
+    // ties, so it starts one level on; equal progress then favours the younger wave
+    if (psh == 3u && (__builtin_amdgcn_s_getreg((3 << 11) | 4) & 1u) == 0u) plev = 1;
+    if (plev == 0) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(2);
     for (;;) {
       STAMP(-1);
       // ---- who proposes this round
