@@ -12,13 +12,15 @@ mu = 2.63815853 (grid_chain_sec11.py:33,171-179).  ``--scaling weak`` gives ever
 
 A bench "step" is one kernel launch that advances every chain by --inner counted flip
 steps (valid proposals, MarkovChain counter increments); value = counted flip steps of
-all chains on all ranks / max-over-ranks wall time of the K timed launches.  A launch
-lasts as long as its slowest chain: where every chain has its own wave slot (an 8-GPU
-job's 8,192-chain shard, C2) that wait is 10-20% of a 1,000-step launch and shrinks with
-longer launches (profiles/r05/unit_times/, launch_length/).  The reference runs its 10^5
-steps per chain as one loop (grid_chain_sec11.py:342), which the library runs as one
-launch; SURVEY.md §8d's steady state (10^4 warm-up + 10^5 timed steps per chain) is
-measured as --inner 5000 --warmup 2 --steps 20.
+all chains on all ranks / max-over-ranks wall time of the K timed launches.  The default
+--inner 5000 makes every protocol SURVEY.md §8d's: the defaults (--warmup 2 --steps 20)
+time 10^5 steps per chain after 10^4 of warm-up, and the driver's --warmup 5 --steps 20
+time 10^5 after 2.5 x 10^4.  (The reference runs its 10^5 steps per chain as one loop,
+grid_chain_sec11.py:342, which the library runs as one launch; a launch lasts as long as
+its slowest chain, a wait that shrinks with longer launches: profiles/r05/launch_length/.)
+At N = 1 the line also carries "secondary": the same warm-up and timed launch COUNTS at
+1,000 steps per launch (the protocol of rounds 1-5, chains earlier in their burn-in and
+therefore faster), on a fresh set of chains after the headline measurement.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -220,6 +222,37 @@ def parity_check(w, ch, bounds, base, seed, chain_id0, total_steps, n_check, wor
             "mismatches": mism, "oracle_s": round(time.perf_counter() - t0, 2)}
 
 
+def secondary_line(dg, w, chains, init, proposal, bounds, base, seed, lo, inner, warmup, steps):
+    """The same warm-up and timed launch counts at ``inner`` steps per launch on a fresh set
+    of the same chains (the round 1-5 driver protocol at inner = 1,000): chains earlier in
+    their burn-in, reported beside the headline, never as it."""
+    import torch
+
+    from flipcomplexityempirical_amd.chain import Chains
+    ch = Chains(dg, chains, w.k, init, proposal=proposal, pop_bounds=bounds, base=base,
+                seed=seed, chain_id0=lo)
+    for _ in range(warmup):
+        ch.run(inner)
+    s0 = int(ch.stats()["steps"].astype(np.uint64).sum())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(steps):
+        ch.run_async(inner)
+        ch.sync()
+        kms.append(ch.last_kernel_ms())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    s1 = int(ch.stats()["steps"].astype(np.uint64).sum())
+    ch.close()
+    return {"value": (s1 - s0) / dt, "unit": "flip steps/s",
+            "flip_steps_per_chain_per_step": inner, "warmup": warmup, "steps": steps,
+            "ms_per_step": dt * 1e3 / steps, "kernel_ms": float(np.mean(kms)),
+            "protocol": f"{warmup} + {steps} launches of {inner} steps per chain on fresh chains "
+                        f"(timed steps {warmup * inner}-{(warmup + steps) * inner} of each chain: "
+                        f"earlier in the burn-in than the headline)"}
+
+
 def flipwalk_env():
     """FLIPWALK_* overrides active in this process (they change launch plans, not trajectories)."""
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("FLIPWALK_")}
@@ -276,10 +309,13 @@ def pmc_mismatch(prof, identity, kernel_ms, tol=0.10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inner", type=int, default=1000,
+    ap.add_argument("--inner", type=int, default=5000,
                     help="flip steps per chain per launch (see the module docstring)")
+    ap.add_argument("--secondary-inner", type=int, default=1000,
+                    help="N=1: also time the same launch counts at this many steps per launch "
+                         "(the round 1-5 protocol) on fresh chains -> \"secondary\" (0 = off)")
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5", "frank"],
                     help="workload (flipcomplexityempirical_amd/workloads.py); the driver's line "
                          "is the default c3")
@@ -337,6 +373,10 @@ def main():
     # a process group whenever torch.distributed.run launched us, also at world 1 (the RCCL
     # path then runs its collectives over one rank: tests/test_distributed.py)
     launched = "MASTER_ADDR" in os.environ and "WORLD_SIZE" in os.environ
+    if world > 1 and not launched:
+        # every rank would run its shard unsynchronised and rank 0 would report a 1-GPU line
+        raise SystemExit("WORLD_SIZE > 1 without MASTER_ADDR: launch bench.py through "
+                         "torch.distributed.run (or set the rendezvous variables)")
     shard_rank, shard_world = rank, world
     if args.shard:
         if launched:
@@ -562,6 +602,11 @@ def main():
             "mean_bnodes": float(st1_arr["bnodes"].mean()),
             "hist_yields": int(hist_cut.sum()),
         }
+        if world == 1 and not args.shard and args.secondary_inner > 0 and not args.resume \
+                and not args.maps and args.secondary_inner != args.inner:
+            out["secondary"] = secondary_line(dg, w, chains, init, proposal, bounds, base,
+                                              args.seed, lo, args.secondary_inner, args.warmup,
+                                              args.steps)
         if world == 1 and not args.shard and not args.no_cpu_baseline:
             b0 = float(np.ravel(base)[0])
             out["cpu_baseline"] = cpu_baseline(args.config, w.desc, percent, b0, args.seed,

@@ -150,7 +150,7 @@ struct fw_chains {
   unsigned long long* d_hist_b = nullptr;
   uint32_t* d_spill = nullptr;
   int32_t* d_next = nullptr;
-  uint32_t* d_gscr = nullptr;  // chain kernel, 3-bit labels: search marks
+  uint32_t* d_gscr = nullptr;  // chain kernel, 5-bit labels: search marks
   int32_t* d_segdone = nullptr;  // finished slices per work unit (launch_slices)
   uint64_t max_yields = 0;  // upper bound on any chain's yield count (maps need < 2^32)
   bool gcache_ok = false;   // the label records' group sums and the stats' cut / bnodes /
@@ -695,10 +695,11 @@ int fw_chains_create(fw_graph* g, int32_t n_chains, int32_t k, const int16_t* in
     return fail(FW_ENOMEM, "device allocation failed for %d chains", n_chains);
   }
   p.seg_done = c->d_segdone;
-  // HBM visit marks of the chain kernel's list search (race_search_gscr: 5-bit labels, and
-  // 3-bit labels off grids); 3-bit grids search with race_search_b3, which keeps its marks
-  // in the labels and looks merge candidates up in its visit list, so they get none
-  if (!use16 && (lb == 5 || (lb == 3 && g->gw == 0))) {
+  // HBM visit marks of the chain kernel's list search (race_search_gscr: 5-bit labels only,
+  // which run on padded rows; 3-bit labels run only on grids, whose race_search_b3 keeps its
+  // marks in the labels).  Footprint: 4 B per node per resident workgroup (C4: 9,000 nodes
+  // x 19 x 256 workgroups = 175 MB), beside the equally sized search-list spill buffer.
+  if (!use16 && lb == 5) {
     p.gscr_words = n;  // one 32-bit mark per node (race_search_gscr)
     const size_t gb = sizeof(uint32_t) * (size_t)c->grid * (size_t)p.gscr_words;
     if (hipMalloc(&c->d_gscr, gb) != hipSuccess || hipMemset(c->d_gscr, 0, gb) != hipSuccess) {

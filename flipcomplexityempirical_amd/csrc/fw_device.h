@@ -1208,7 +1208,7 @@ struct Ctx {
   }
 
   // -------------------------------------------------------------- contiguity
-  // -- visit marks in HBM (LB == 5; 3-bit labels off grids): one 32-bit word per node in
+  // -- visit marks in HBM (LB == 5 only: 3-bit labels run on grids, race_search_b3): one 32-bit word per node in
   // this workgroup's slice of gscr, 0 = unvisited, 1 + source index, ~0 = v.  A claim is
   // ONE compare-and-swap that returns the mark it found (the class of an already visited
   // node): no separate load and no retry loop, as 4-bit marks sharing a word needed
@@ -1236,6 +1236,10 @@ struct Ctx {
   // index << 28), so the node's mark is never read back.
   __device__ bool race_search_gscr(int v, uint32_t a, int m, int src, uint64_t cls,
                                    uint64_t& bfs_nodes, uint64_t& bfs_deg) {
+    // one 16-lane group per node: a CSR row past 16 entries would lose neighbours 16 and up,
+    // so only padded rows (E16: max degree <= 16) and grids (slots 0..3) may use it; node
+    // ids live in bits 0..27 of a list entry (fw_chains_create: n <= 65,536, G <= 1,024)
+    static_assert(E16 || GRID, "race_search_gscr: padded 16-wide rows or grids only");
     constexpr uint32_t XM = (1u << 28) - 1u;
     if (lane == 0) gm_set(v, ~0u);  // v: never a class (any m, up to the row's 16 sources)
     if (lane < m) {
@@ -2196,7 +2200,7 @@ struct Ctx {
     bool verdict;
     if constexpr (LB == 3 && GRID)
       verdict = race_search_b3(v, a, m, src, cls, scap, rs, bfs_nodes, bfs_deg);
-    else if constexpr (LB == 3 || LB == 5)
+    else if constexpr (LB == 5)
       verdict = race_search_gscr(v, a, m, src, cls, bfs_nodes, bfs_deg);
     else
       verdict = race_search(v, a, m, src, cls, bfs_nodes, bfs_deg);

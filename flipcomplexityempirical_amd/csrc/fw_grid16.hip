@@ -212,9 +212,6 @@ __device__ __forceinline__ uint32_t low_bytes(int t) {  // 0xFF in bytes 0..t-1
   const uint32_t tc = (uint32_t)min(max(t, 0), 4);
   return tc == 4u ? 0xFFFFFFFFu : (1u << (8u * tc)) - 1u;
 }
-__device__ __forceinline__ uint32_t byte_clear(int t) {  // all bytes but byte t (t in 0..3)
-  return (uint32_t)t < 4u ? ~(0xFFu << (8 * t)) : 0xFFFFFFFFu;
-}
 // per byte: 0x80 where the one-hot bytes a and b differ (different labels)
 __device__ __forceinline__ uint32_t ne_bytes(uint32_t a, uint32_t b) {
   return ~((a & b) + 0x7F7F7F7Fu) & 0x80808080u;
@@ -245,14 +242,19 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
   // which of the four nodes have each neighbour (W >= 4: at most one row wrap, at tw)
   const int r0 = gd(x0);
   const int c0 = x0 - mulW(r0, W);
-  const int tw = W - c0;  // first byte on the next grid row (>= 4: none)
+  const int tw = W - c0;  // first byte on the next grid row (>= 4: none); >= 1
+  // byte masks from 64-bit shifts of constants (a shift by 32 empties the low dword): the
+  // bytes on the next grid row, the column-0 bytes (byte tw, or byte 0 when c0 == 0) and the
+  // column-(W-1) byte (byte tw - 1 when tw <= 4).  Bytes past n (row H and beyond) are
+  // cleared by mN, so row H - 1 may clear its next-row bytes too.  Equal to the per-byte
+  // clamp/select form after the & mN on every grid W >= 4, H <= 40, all groups (host check).
+  const uint32_t t8 = (uint32_t)min(tw, 4) << 3;
+  const uint32_t nxt = (uint32_t)(~0ull << t8);
   const uint32_t mN = low_bytes(n - x0);
-  const uint32_t lowtw = low_bytes(tw);
-  const uint32_t mU = r0 == 0 ? ~lowtw : 0xFFFFFFFFu;
-  uint32_t mD = r0 == H - 1 ? ~lowtw : 0xFFFFFFFFu;
-  mD = r0 + 1 == H - 1 ? lowtw : mD;
-  const uint32_t mL = byte_clear(c0 == 0 ? 0 : tw);
-  const uint32_t mR = byte_clear(tw - 1);
+  const uint32_t mU = r0 > 0 ? 0xFFFFFFFFu : nxt;
+  const uint32_t mD = r0 < H - 2 ? 0xFFFFFFFFu : (r0 == H - 2 ? ~nxt : 0u);
+  const uint32_t mL = ~((uint32_t)(0xFFull << t8) | (c0 == 0 ? 0xFFu : 0u));
+  const uint32_t mR = ~(uint32_t)(0xFFull << (((uint32_t)min(tw, 5) << 3) - 8u));
   if constexpr (MODE != FW_PROPOSE_CUTEDGE) {
     const uint32_t bits = (U & mU) | (L & mL) | (R & mR) | (Dn & mD);
     w4 = byte_popc(bits & ~O & mN);
@@ -957,33 +959,48 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
 
       STAMP(0);  // draw
       // ---- select, level 1: group sums (PER per lane, read as PER/2 u16 pairs)
-      uint32_t gs[PER];
+      uint32_t w2[PER / 2];
       uint32_t s = 0;
 #pragma unroll
       for (int t = 0; t < PER / 2; ++t) {
-        const int wi = q * (PER / 2) + t;
-        const uint32_t w2 = lvl1[wi];  // words past GW (SG) are zero padding
-        gs[2 * t] = w2 & 0xFFFFu;
-        gs[2 * t + 1] = w2 >> 16;
-        s += gs[2 * t] + gs[2 * t + 1];
+        w2[t] = lvl1[q * (PER / 2) + t];  // words past GW (SG) are zero padding
+        s += (w2[t] & 0xFFFFu) + (w2[t] >> 16);
+      }
+      // packed u16 prefixes of the lane's groups, pair t = (c_{2t+1}, c_{2t+2}) with c_j the
+      // sum of its first j groups (< 2^15 on the chosen lane: <= 16 groups of <= 64 x 4, or
+      // BIG's <= 4 supergroups of <= 16 x 192); independent of r, so they fill the scan's
+      // DPP wait states
+      uint32_t pp[PER / 2];
+      {
+        uint32_t base = 0;
+#pragma unroll
+        for (int t = 0; t < PER / 2; ++t) {
+          pp[t] = __umul24(base, 0x10001u) + (w2[t] + (w2[t] << 16));
+          base = pp[t] >> 16;
+        }
       }
       const uint32_t incl = row_scan(s);
       const uint32_t rb1 = rowbits(ballot(incl > r), row);
       const int Lw = __ffs(rb1) - 1;
-      // the group holding rank rl among this lane's PER: the count of inclusive prefixes
-      // <= rl, and the last such prefix (prefixes are non-decreasing)
+      // the group holding rank rl among this lane's PER (only lane Lw's, where 0 <= rl < s,
+      // is used): e_j = rl - c_j in u16 arithmetic wraps past 2^15 exactly when c_j > rl, so
+      // the groups before it are the prefixes that do not wrap and the remaining rank is
+      // min(rl, the smallest e_j) -- packed u16 ops, no compare / carry chain
       const uint32_t rl = r - (incl - s);
-      uint32_t c1 = 0, before = 0, tfu = 0;
+      typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+      const u16x2 rl2 = __builtin_bit_cast(u16x2, __umul24(rl & 0xFFFFu, 0x10001u));
+      u16x2 mn = {0xFFFFu, 0xFFFFu}, wraps = {0u, 0u};
 #pragma unroll
-      for (int t = 0; t < PER; ++t) {
-        c1 += gs[t];
-        const bool le = c1 <= rl;
-        tfu += le ? 1u : 0u;
-        before = le ? c1 : before;
+      for (int t = 0; t < PER / 2; ++t) {
+        const u16x2 e = rl2 - __builtin_bit_cast(u16x2, pp[t]);
+        mn = __builtin_elementwise_min(mn, e);
+        wraps += e >> (uint16_t)15;
       }
-      const int tf = min((int)tfu, PER - 1);
+      const uint32_t rem = min(rl, (uint32_t)min(mn.x, mn.y));
+      const int tfu = PER - (int)wraps.x - (int)wraps.y;
+      const int tf = min(tfu, PER - 1);
       // pack (group, remaining rank) into one row broadcast
-      const uint32_t pk1 = row_pick(((uint32_t)(q * PER + tf) << 16) | ((rl - before) & 0xFFFFu), Lw, q);
+      const uint32_t pk1 = row_pick(((uint32_t)(q * PER + tf) << 16) | (rem & 0xFFFFu), Lw, q);
       int gi;
       uint32_t r1;
       uint32_t rbg = 1u;
@@ -1045,7 +1062,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       if constexpr (LB == 2) {
         // one unconditional read per lane (cells off the grid read v and are masked)
         const int xr = vr + my_dr, xc = vc + my_dc;
-        const bool inb = (q <= 12) & (xr >= 0) & (xr < H) & (xc >= 0) & (xc < W);
+        const bool inb = (q <= 12) & ((uint32_t)xr < (uint32_t)H) & ((uint32_t)xc < (uint32_t)W);
         const int xx = mulW(xr, W) + xc;
         const uint32_t l0 = P::get(lab, inb ? xx : v);
         h.x = inb ? xx : -1;
@@ -1200,7 +1217,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
 #pragma unroll
         for (int t = 0; t < 3; ++t) {  // branch-free: all three reads issued, then masked
           const int rr = vr + win_dr[t], cw = vc + win_dc[t];
-          inw[t] = (rr >= 0) & (rr < H) & (cw >= 0) & (cw < W);
+          inw[t] = ((uint32_t)rr < (uint32_t)H) & ((uint32_t)cw < (uint32_t)W);
           lw[t] = P::get(lab, inw[t] ? mulW(rr, W) + cw : v);
         }
 #pragma unroll
@@ -1462,6 +1479,11 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
         }
       }
       STAMP(9);  // commit
+      // 1/|B'| by a select every lane executes: the table load completes here, before the
+      // observation's histogram flush atomics, and its register is free for the next
+      // iteration (consumed inside the exec-masked branch, a later reuse of that register
+      // waited on vmcnt(0) -- for the flush atomics issued after it as well)
+      invb = accepted ? invb_new : invb;
       if (accepted) {
         n_acc += 1;
         if (FULL && p.sched) sched_row(n_acc);
@@ -1470,7 +1492,6 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
         cut += dcut;
         bnodes += plus - minus;
         n_bchg += (uint32_t)(plus + minus);
-        invb = invb_new;
         if ((uint32_t)q == a) pops -= pv;
         if ((uint32_t)q == d) pops += pv;
         if (rule == FW_ACCEPT_BOUNDARY && p.flags[v]) {

@@ -51,7 +51,7 @@ struct FwRunParams {
   unsigned long long* hist_cut;  // [nedges+1+FW_HIST_PAD]
   unsigned long long* hist_b;    // [n+1+FW_HIST_PAD]
   uint32_t* spill;             // [grid][n] search-list spill
-  uint32_t* gscr;              // race_search_gscr (5-bit labels; 3-bit off grids): [grid][n] 32-bit visit marks (zero)
+  uint32_t* gscr;              // race_search_gscr (5-bit labels, padded rows): [grid][n] 32-bit visit marks (zero)
   int32_t gscr_words;
   int32_t* next_chain;         // dynamic chain counter (zeroed before launch)
   int32_t* trace;              // optional [n_chains][steps]: v*64+target if accepted, -1 if not

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   C.wts = reinterpret_cast<LDS uint32_t*>(sm + p.off_w);
   C.list = reinterpret_cast<LDS uint32_t*>(sm + p.off_list);
   C.spill = (GLB uint32_t*)(p.spill + (size_t)blockIdx.x * (size_t)p.g.n);
-  C.gscr = (LB == 3 || LB == 5) && p.gscr ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
+  C.gscr = LB == 5 && p.gscr ? (GLB uint32_t*)(p.gscr + (size_t)blockIdx.x * (size_t)p.gscr_words) : nullptr;
   C.qcap = p.qcap;
   C.scap = min(128, (p.off_list - p.off_gsum) / 4);
   C.k = p.k;

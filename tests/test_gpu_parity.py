@@ -482,9 +482,10 @@ def test_chain_kernel_5bit_labels(gpu_lib, name, lb, cap, monkeypatch):
 @pytest.mark.parametrize("search", ["bitboard", "list"])
 def test_chain_kernel_3bit_labels(gpu_lib, name, search, monkeypatch):
     """The one-chain-per-wave kernel with 3-bit labels (FLIPWALK_CSR_LB=3; the default on
-    large grids with k <= 8): labels straddle bytes, and the list search keeps its visit
-    marks in HBM instead of in the labels (list: forced for every exact search, with a
-    2-entry LDS list so the visit list spills too)."""
+    large grids with k <= 8): labels straddle bytes, and the list search (race_search_b3)
+    keeps its visit marks in the labels as borrowed class codes, with no HBM mark array
+    (list: forced for every exact search, with a 2-entry LDS list so the visit list spills
+    too)."""
     monkeypatch.setenv("FLIPWALK_NO_GRID16", "1")
     monkeypatch.setenv("FLIPWALK_CSR_LB", "3")
     if search == "list":
