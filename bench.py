@@ -136,19 +136,28 @@ def cpu_baseline(name, desc, percent, base, seed, seconds=10.0, workers=None):
     return out
 
 
-def native_cpu_baseline(w, bounds, base, seed, seconds=10.0, workers=None):
+def native_cpu_baseline(w, bounds, base, seed, seconds=10.0, workers=None, lo=0, chains=1):
     """The C oracle (oracle/flipchain_oracle.c), one chain per thread on every usable core
-    (ctypes releases the GIL), each chain advanced in 5,000-step calls until the deadline."""
+    (ctypes releases the GIL), each chain advanced in 5,000-step calls until the deadline.
+    Worker k runs the benched chain lo + i_k, i_k spread evenly over the line's ``chains``,
+    with that chain's own base (``base``: one value or one per benched chain), so a base
+    ladder (C5) is sampled across its bases."""
     from concurrent.futures import ThreadPoolExecutor
 
     from flipcomplexityempirical_amd.chain import PROPOSALS, metropolis_table
     from oracle import oracle as O
     workers = workers or host_cores()[0]
-    thr = metropolis_table(base, w.graph.maxdeg)
-    mode = PROPOSALS[w.proposal]
+    bases = np.broadcast_to(np.asarray(base, np.float64), (max(1, chains),))
+    mode = PROPOSALS[w.proposal] if isinstance(w.proposal, str) else int(w.proposal)
+    init = np.asarray(w.init, np.int16)
+    pick = np.linspace(0, max(1, chains) - 1, workers).round().astype(int)
 
-    def one(cid):
-        lab, st = w.init.copy(), O.new_stats(1)
+    def one(k):
+        i = int(pick[k])
+        cid = lo + i
+        thr = metropolis_table(float(bases[i]), w.graph.maxdeg)
+        lab = (init if init.ndim == 1 else init[i]).copy()
+        st = O.new_stats(1)
         lab, st, _, _ = O.run_chain(w.graph, lab, w.k, mode, *bounds, thr, seed, cid, 100, stats=st)
         t0 = time.perf_counter()
         s0 = int(st["steps"][0])
@@ -163,7 +172,9 @@ def native_cpu_baseline(w, bounds, base, seed, seconds=10.0, workers=None):
     out = {"value": rate, "unit": "flip steps/s", "kind": "port",
            "sample": f"C oracle (oracle/flipchain_oracle.c, the bit-exact restatement), "
                      f"{workers} chains x ~{seconds:.0f}s, one chain per thread on every usable "
-                     f"host core, same workload; {sum(s for s, _ in res)} steps total"}
+                     f"host core, same workload (chains spread over the line's {chains}, each "
+                     f"with its own base, from the seed plan); {sum(s for s, _ in res)} steps "
+                     f"total"}
     out.update(_host_fields(workers))
     out["per_core"] = rate / workers
     out["extrapolated_all_cpus"] = rate / workers * out["cpu_count"]
@@ -607,12 +618,18 @@ def main():
             out["secondary"] = secondary_line(dg, w, chains, init, proposal, bounds, base,
                                               args.seed, lo, args.secondary_inner, args.warmup,
                                               args.steps)
-        if world == 1 and not args.shard and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             b0 = float(np.ravel(base)[0])
-            out["cpu_baseline"] = cpu_baseline(args.config, w.desc, percent, b0, args.seed,
-                                               seconds=args.cpu_seconds)
-            out["cpu_native"] = native_cpu_baseline(w, bounds, b0, args.seed,
-                                                    seconds=args.cpu_seconds)
+            if not args.shard:
+                out["cpu_baseline"] = cpu_baseline(args.config, w.desc, percent, b0, args.seed,
+                                                   seconds=args.cpu_seconds)
+            # every line (shards too): the native C path on the host cores, and the GPU's
+            # rate over it extrapolated to every hardware thread of the host
+            out["cpu_native"] = native_cpu_baseline(w, bounds, base, args.seed,
+                                                    seconds=args.cpu_seconds, lo=lo,
+                                                    chains=chains)
+            out["cpu_native"]["gpu_over_all_cpus"] = (
+                out["value"] / out["cpu_native"]["extrapolated_all_cpus"])
         print(json.dumps(out), flush=True)
     ch.close()
     dg.close()

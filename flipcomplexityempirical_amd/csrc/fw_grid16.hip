@@ -286,22 +286,25 @@ __device__ __forceinline__ uint32_t bsum4m(uint32_t v) { return (v * 0x01010101u
 // of sources in one window component are equal and other fills disjoint, so the
 // sequential verdict is order-free: 1 if some fill holds every source, else 0 if some
 // fill touches no border, else -1 (undecided).  Row-uniform result.
-__device__ __forceinline__ int window_verdict_row(uint64_t A, int q, int row, bool need, uint32_t& nflood) {
+// Layout: window row r (0..6, v's row 3) in byte r, column c (0..6, v's column 3) at bit c;
+// bit 7 of every byte is a zero guard column, so a dilation needs no column masks (a shift
+// into the guard is removed by & A): 4 shifts, 2 ORs of three and one AND per 32-bit half.
+__device__ __forceinline__ int window_verdict8(uint64_t A, int q, int row, bool need, uint32_t& nflood) {
 #ifdef FW_STAMPS
 #define FLOOD_COUNT ++nflood
 #else
 #define FLOOD_COUNT
 #endif
-  const uint64_t C0 = 0x0040810204081ull, C6 = C0 << 6;
-  const uint64_t BORDER = C0 | C6 | 0x7Full | (0x7Full << 42);
-  const uint64_t src = A & ((1ull << 17) | (1ull << 23) | (1ull << 25) | (1ull << 31));
-  const int sb = q == 0 ? 17 : q == 1 ? 23 : q == 2 ? 25 : 31;
+  constexpr uint64_t BORDER = 0x7Full | (0x7Full << 48) | 0x0001010101010101ull | 0x0040404040404040ull;
+  // sources up (row 2, column 3), left (3, 2), right (3, 4), down (4, 3)
+  const uint64_t src = A & ((1ull << 19) | (1ull << 26) | (1ull << 28) | (1ull << 35));
+  const int sb = q == 0 ? 19 : q == 1 ? 26 : q == 2 ? 28 : 35;
   uint64_t x = (need && q < 4) ? src & (1ull << sb) : 0ull;
   if (x) {
     // two dilations per convergence test (same fixpoint, half the loop-exit tests)
     for (;;) {
-      const uint64_t y = (x | ((x << 1) & ~C0) | ((x >> 1) & ~C6) | (x >> 7) | (x << 7)) & A;
-      x = (y | ((y << 1) & ~C0) | ((y >> 1) & ~C6) | (y >> 7) | (y << 7)) & A;
+      const uint64_t y = (x | (x << 1) | (x >> 1) | (x << 8) | (x >> 8)) & A;
+      x = (y | (y << 1) | (y >> 1) | (y << 8) | (y >> 8)) & A;
       FLOOD_COUNT;
       if (x == y) break;
     }
@@ -649,14 +652,6 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
                             : q == 3 ? (1u << 11) | (1u << 5) | (1u << 6)
                             : q == 4 ? (1u << 12) | (1u << 6) | (1u << 7)
                                      : 0u;
-  // 7x7 window cells of this lane (three per lane, v skipped): offsets from v
-  int win_dr[3], win_dc[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int pos = window_pos(q + ROW * t);
-    win_dr[t] = pos / 7 - 3;
-    win_dc[t] = pos % 7 - 3;
-  }
   auto divmod = [&](int x, int& r, int& c) {
     r = gd(x);
     c = x - mulW(r, W);
@@ -1210,22 +1205,26 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       // bitwise, not short-circuit: no exec-mask branches
       bool contig = (m == 1) | ((m >= 2) & (m - (lNE + lES + lSW + lWN) <= 1));
       bool need = go & pop_ok & (m >= 2) & !contig;
-      if (ballot(need)) {  // 7x7 window flood fill (3 window cells per row-lane)
+      if (ballot(need)) {  // 7x7 window flood fill (window_verdict8's layout)
+        // read t: row-lane q takes window row 2t + q / 8, column q % 8 (column 7: the guard,
+        // never a cell), so row ballot t is bits 16t .. 16t + 15 of A
         uint64_t A = 0;
-        bool inw[3];
-        uint32_t lw[3];
+        bool inw[4];
+        uint32_t lw[4];
+        const int wcol = q & 7;
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {  // branch-free: all three reads issued, then masked
-          const int rr = vr + win_dr[t], cw = vc + win_dc[t];
-          inw[t] = ((uint32_t)rr < (uint32_t)H) & ((uint32_t)cw < (uint32_t)W);
+        for (int t = 0; t < 4; ++t) {  // branch-free: all four reads issued, then masked
+          const int wrow = 2 * t + (q >> 3);
+          const int rr = vr + wrow - 3, cw = vc + wcol - 3;
+          inw[t] = (wcol < 7) & (wrow < 7) & ((uint32_t)rr < (uint32_t)H) & ((uint32_t)cw < (uint32_t)W);
           lw[t] = P::get(lab, inw[t] ? mulW(rr, W) + cw : v);
         }
 #pragma unroll
-        for (int t = 0; t < 3; ++t)
+        for (int t = 0; t < 4; ++t)
           A |= (uint64_t)rowbits(ballot(inw[t] & (lw[t] == a)), row) << (ROW * t);
-        A = (A & ((1ull << 24) - 1ull)) | ((A >> 24) << 25);
+        A &= ~(1ull << 27);  // v (row 3, column 3)
         uint32_t nflood = 0;
-        const int wvd = window_verdict_row(A, q, row, need, nflood);
+        const int wvd = window_verdict8(A, q, row, need, nflood);
         STAMP_COUNT(12, 1);
         STAMP_COUNT(13, __builtin_amdgcn_readfirstlane(__reduce_max_sync(~0ull, nflood)));
         if (wvd >= 0) {
@@ -1483,6 +1482,9 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       // observation's histogram flush atomics, and its register is free for the next
       // iteration (consumed inside the exec-masked branch, a later reuse of that register
       // waited on vmcnt(0) -- for the flush atomics issued after it as well)
+      // (the empty asm reads the loaded value in every lane, so its wait cannot sink into
+      // the accepted-rows branch)
+      asm volatile("" ::"v"(invb_new));
       invb = accepted ? invb_new : invb;
       if (accepted) {
         n_acc += 1;
