@@ -512,6 +512,41 @@ __device__ int grid_race_bb(const LDS uint8_t* lab, int n, int W, int H, int lan
   uint32_t V = F[0] | F[1] | F[2] | F[3];
   int verdict = -1;
   uint32_t P;  // processed cells
+  if (n_classes() == 2) {
+    // two classes after the ring links (most searches): one frontier per class, the union
+    // of its directions' frontiers -- dilation and the merge test distribute over unions,
+    // and a class is closed when every direction of it is -- one merge test and two reach
+    // ballots per level; the general loop's levels, stopping rules and counters
+    // (grid_race_bb2's two-class path on this 32-column window)
+    uint32_t fa = 0u, fb = 0u;
+    int ra = -1;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!((am4 >> d) & 1u)) continue;
+      const int rep = __ffs((M >> (4 * d)) & 15u) - 1;
+      if (ra < 0) ra = rep;
+      if (rep == ra)
+        fa |= F[d];
+      else
+        fb |= F[d];
+    }
+    for (;;) {
+      if (ballot(((fa | fb) & E) != 0u)) return -1;
+      const uint32_t da = dilate32(fa) & A, db = dilate32(fb) & A;
+      const uint32_t nw = (da | db) & ~V;
+      const bool met = ballot((da & (fb | (db & nw))) != 0u) != 0ull;
+      fa = da & nw;
+      fb = db & nw;
+      // met: connected; a class with no new cell: closed, disconnected.  Either way the
+      // processed cells are the visited ones before this level's new cells.
+      if (met || !ballot(fa != 0u) || !ballot(fb != 0u)) {
+        verdict = met ? 1 : 0;
+        break;
+      }
+      V |= nw;
+    }
+    P = V;
+  } else
   for (;;) {
     const uint32_t lvl = F[0] | F[1] | F[2] | F[3];
     if (n_classes() == 1) {

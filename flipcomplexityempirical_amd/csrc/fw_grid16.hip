@@ -1577,9 +1577,19 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
   STAMP_FLUSH
 }
 
+// Register budgets.  The kernel holds 48 chains per CU at 3 waves per SIMD, which LDS and
+// 168 VGPRs allow together; its search paths want a few more registers, so the default
+// instantiation is held to 3 waves per SIMD (a few VGPRs spilled, outside the hot path:
+// C3 +0.8%, +2% at 15,000-35,000 steps, profiles/r06/ab/ab_*_v6.jsonl) and a second lean
+// one (W2) keeps every register, at 2 waves per SIMD, for launches with no more than 2
+// waves of work per SIMD (the 8-GPU job's 8,192-chain shards: +4.6%).
 template <int LB, int MODE, int PER, bool FULL, bool BIG>
-__global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_kernel(FwRunParams p) {
+__global__ __launch_bounds__(64 * MAX_NW) __attribute__((amdgpu_waves_per_eu(3))) void fw_grid16_kernel(FwRunParams p) {
   grid16_body<LB, MODE, PER, FULL, BIG, 1>(p);
+}
+template <int LB, int MODE, int PER>
+__global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_w2_kernel(FwRunParams p) {
+  grid16_body<LB, MODE, PER, false, false, 1>(p);
 }
 
 // speculative attempts: R rows per chain.  A 3-waves-per-SIMD register budget (168 VGPRs:
@@ -1620,6 +1630,17 @@ void* pick16(int G) {
       case 10: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL, false>);
       default: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL, false>);
     }
+  }
+}
+
+template <int MODE>
+void* pick16_w2(int G) {
+  if (is_big(G)) return nullptr;
+  switch (per16(G)) {
+    case 2: return reinterpret_cast<void*>(&fw_grid16_w2_kernel<2, MODE, 2>);
+    case 4: return reinterpret_cast<void*>(&fw_grid16_w2_kernel<2, MODE, 4>);
+    case 10: return reinterpret_cast<void*>(&fw_grid16_w2_kernel<2, MODE, 10>);
+    default: return reinterpret_cast<void*>(&fw_grid16_w2_kernel<2, MODE, 16>);
   }
 }
 
@@ -1708,8 +1729,19 @@ int fw_grid16_launch_rows(const FwRunParams& p) { return grid16_full(p) ? 1 : p.
 // which the R = 1 kernels (FULL features on) fill with nw / spec waves of four chains
 int fw_grid16_launch_nw(const FwRunParams& p) { return p.nw * fw_grid16_launch_rows(p) / p.spec; }
 
+// the W2 instantiation (2-bit labels, small grids, lean, R = 1)
+static void* grid16_fn_w2(const FwRunParams& p) {
+  if (p.lb != 2) return nullptr;
+  return p.mode == FW_PROPOSE_CUTEDGE ? pick16_w2<FW_PROPOSE_CUTEDGE>(p.G)
+                                      : pick16_w2<FW_PROPOSE_PAIRS>(p.G);
+}
+
 static void* grid16_fn_r(const FwRunParams& p, bool full, int R) {
   if (full) return pick16_mode<true>(p);
+  if (R == 1 && p.w2) {
+    void* f = grid16_fn_w2(p);
+    if (f) return f;
+  }
   if (R == 2) return pick16_spec_mode<2>(p);
   if (R == 4) return pick16_spec_mode<4>(p);
   return pick16_mode<false>(p);
@@ -1728,6 +1760,7 @@ void* fw_grid16_fn(const FwRunParams& p) {
 // that an attempt leaves the state unchanged (C3), x the measured per-row speed of the R > 1
 // kernels.  Ties: R = 1, then fewer waves.  FLIPWALK_SPEC=1/2/4 forces R.
 int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
+  p.w2 = 0;  // chosen below, once the plan's rows and waves are known
   // slot: labels | u16 group sums (16 x PER per row; BIG: padded to whole supergroups) |
   // BIG: u16 supergroup sums (16 x PER)
   const bool big = is_big(p.G);
@@ -1818,13 +1851,53 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
     }
   }
   if (best_nw == 0) return -1;
+  // W2: with no more than 2 waves of work per SIMD the lean R = 1 kernel runs under the
+  // 2-waves-per-SIMD register budget (no spills; FLIPWALK_W2=0 / 1 forbids / forces it)
+  p.w2 = 0;
+  {
+    const char* ew = getenv("FLIPWALK_W2");
+    const int want = ew && ew[0] ? atoi(ew) : -1;
+    void* fw2 = (best_r == 1 && !full && want != 0) ? grid16_fn_w2(p) : nullptr;
+    const long long quads = (p.n_chains + 3) / 4;
+    const int cus = prop.multiProcessorCount;
+    if (fw2 && (want == 1 || quads <= 2ll * 4 * cus)) {
+      int w_nw = 0, w_blocks = 0, w_lds = 0;
+      long long w_busy = -1;
+      for (int nw = 1; nw <= MAX_NW; ++nw) {
+        if (force_nw && nw != force_nw) continue;
+        const int lds = LDS_GUARD + 4 * nw * stride + p.scr_bytes + 4 * p.qcap16;
+        if (lds > 160 * 1024 - 256) break;
+        if (hipFuncSetAttribute(fw2, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+          return -1;
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fw2, 64 * nw, (size_t)lds) !=
+                hipSuccess || per_cu <= 0)
+          continue;
+        const long long wgs = (quads + nw - 1) / nw;
+        const long long busy = wgs > (long long)per_cu * cus ? -1 : ((wgs + cus - 1) / cus * nw + 3) / 4;
+        if (busy < 0) continue;  // W2 must hold all the work in one round
+        if (w_nw == 0 || busy < w_busy) {
+          w_nw = nw;
+          w_blocks = per_cu;
+          w_lds = lds;
+          w_busy = busy;
+        }
+      }
+      if (w_nw) {
+        p.w2 = 1;
+        best_nw = w_nw;
+        best_blocks = w_blocks;
+        best_lds = w_lds;
+      }
+    }
+  }
   p.spec = best_r;
   p.nw = best_nw;
   const int cpw = 4 / best_r;
   p.off_scr = LDS_GUARD + cpw * best_nw * stride;
   p.off_list16 = p.off_scr + p.scr_bytes;
   p.lds16 = best_lds;
-  // both the lean kernel of the plan and the FULL one (features switched on later)
+  // both the lean kernel of the plan (W2 or not) and the FULL one (features switched on later)
   for (int f = 0; f < 2; ++f) {
     void* fn = grid16_fn_r(p, f == 1, f == 1 ? 1 : best_r);
     if (fn && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, best_lds) != hipSuccess)
@@ -1832,10 +1905,10 @@ int fw_grid16_plan(FwRunParams& p, int device, int* grid) {
   }
   const char* verbose = getenv("FLIPWALK_VERBOSE");
   if (verbose && verbose[0] == '1')
-    fprintf(stderr, "flipwalk: grid kernel %s, %d-bit labels, %d row(s) per chain, LDS %d B per "
+    fprintf(stderr, "flipwalk: grid kernel %s%s, %d-bit labels, %d row(s) per chain, LDS %d B per "
             "workgroup of %d waves, %d workgroups (%d chains) per CU\n",
-            is_big(p.G) ? "large-grid plan" : "small-grid plan", p.lb, best_r, best_lds, best_nw,
-            best_blocks, best_blocks * best_nw * cpw);
+            is_big(p.G) ? "large-grid plan" : "small-grid plan", p.w2 ? " (W2 register budget)" : "",
+            p.lb, best_r, best_lds, best_nw, best_blocks, best_blocks * best_nw * cpw);
   const long long per_wg = (long long)cpw * best_nw;
   long long gsz = (long long)best_blocks * prop.multiProcessorCount;
   const long long need = (p.n_chains + per_wg - 1) / per_wg;

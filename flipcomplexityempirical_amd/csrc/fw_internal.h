@@ -76,6 +76,8 @@ struct FwRunParams {
   int32_t slot_stride;         // bytes between chain slots
   int32_t nw;                  // waves per workgroup (of the plan's lean kernel)
   int32_t spec;                // rows per chain of the lean kernel (speculative attempts: 1, 2, 4)
+  int32_t w2;                  // 1: the lean R = 1 kernel under a 2-waves-per-SIMD register budget
+                               // (launches with at most 2 waves of work per SIMD: fw_grid16_plan)
   int32_t off_scr, scr_bytes;  // 4-bit search scratch
   int32_t off_list16, qcap16;  // shared visit list
   int32_t no_bb;               // 1: exact searches skip the bitboard form (tests)

@@ -163,6 +163,31 @@ def test_many_chains_per_workgroup(gpu_lib, name, bitboard, monkeypatch):
     assert st["bfs_runs"].sum() > 0
 
 
+W2_GRIDS = ["grid10_k2_bi", "grid12_k4_pairs", "grid12_k4_cut", "grid20_k4_mu", "grid11x13_k4",
+            "grid30x18_k2_bi"]
+
+
+@pytest.mark.parametrize("w2", ["0", "1"])
+@pytest.mark.parametrize("name", W2_GRIDS)
+@pytest.mark.parametrize("bitboard", [True, False])
+def test_grid_kernel_register_budgets(gpu_lib, name, w2, bitboard, monkeypatch):
+    """Both register budgets of the lean grid kernel (fw_grid16_plan): the default one held to
+    3 waves per SIMD (FLIPWALK_W2=0) and W2, 2 waves per SIMD, which the plan takes for
+    launches with at most 2 waves of work per SIMD (every small test, the 8-GPU job's
+    8,192-chain shards): plans, counters, sums and histograms equal the oracle's, with
+    exact searches in the bitboard form (its two-class path included) and as the list
+    search."""
+    monkeypatch.delenv("FLIPWALK_NO_GRID16", raising=False)
+    monkeypatch.setenv("FLIPWALK_W2", w2)
+    if bitboard:
+        monkeypatch.delenv("FLIPWALK_NO_BITBOARD", raising=False)
+    else:
+        monkeypatch.setenv("FLIPWALK_NO_BITBOARD", "1")
+    case = {c.name: c for c in CASES}[name]
+    st = _run_vs_oracle(case, 45, [400, 300])
+    assert (st["accepts"] > 0).all()
+
+
 @pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
                                        ("grid30x18_k2_bi", "auto"), ("sec11_a2_k2", "auto"),
                                        ("tract_k4", "auto")])
