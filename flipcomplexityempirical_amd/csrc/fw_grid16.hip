@@ -221,7 +221,7 @@ __device__ __forceinline__ uint32_t byte_popc(uint32_t f) {  // per-byte popcoun
   return (t & 0x33333333u) + ((t >> 2) & 0x33333333u);
 }
 
-template <int MODE, bool NEED_CD>
+template <int MODE, bool NEED_CD, bool BATCH = true>
 __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, int W, int H, int n,
                                               GDiv gd, uint32_t& w4, uint32_t& cd4) {
   w4 = 0;
@@ -230,15 +230,20 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
   // all-zero for a group tail past n)
   const int xs = x0 < n ? x0 : 0;
   const bool hasU = xs + 3 - W >= 0, hasD = xs + W < n;
-  const uint32_t own = lab_window<2>(lab, xs);  // fields x0-1 .. x0+4
-  const uint32_t up0 = lab_window<2>(lab, hasU ? xs - W : xs);
-  const uint32_t dn0 = lab_window<2>(lab, hasD ? xs + W : xs);
-  const uint32_t up = hasU ? up0 : 0u, dn = hasD ? dn0 : 0u;
-  const uint32_t o_lo = onehot4(spread4(own)), o_hi = onehot4(spread4(own >> 8));
-  const uint32_t L = o_lo;                                     // x-1
-  const uint32_t O = __builtin_amdgcn_alignbyte(o_hi, o_lo, 1);  // x
-  const uint32_t R = __builtin_amdgcn_alignbyte(o_hi, o_lo, 2);  // x+1
-  const uint32_t U = onehot4(spread4(up >> 2)), Dn = onehot4(spread4(dn >> 2));
+  // the three windows' dword pairs (lab_window: fields x-1 .. x+4), all loaded before any
+  // is used -- one LDS round trip; at the register limit the scheduler otherwise waits for
+  // each pair before issuing the next -- with the edge masks computed while they land
+  const LDS uint32_t* lw32 = reinterpret_cast<const LDS uint32_t*>(lab);
+  const int xw[3] = {xs, hasU ? xs - W : xs, hasD ? xs + W : xs};
+  uint32_t wlo[3], whi[3];
+  int wbit[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    wbit[t] = (xw[t] - 1) * 2;
+    const int wi = wbit[t] >> 5;  // arithmetic: -1 for x = 0 (the guard word, masked)
+    wlo[t] = lw32[wi];
+    whi[t] = lw32[wi + 1];
+  }
   // which of the four nodes have each neighbour (W >= 4: at most one row wrap, at tw)
   const int r0 = gd(x0);
   const int c0 = x0 - mulW(r0, W);
@@ -255,6 +260,21 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
   const uint32_t mD = r0 < H - 2 ? 0xFFFFFFFFu : (r0 == H - 2 ? ~nxt : 0u);
   const uint32_t mL = ~((uint32_t)(0xFFull << t8) | (c0 == 0 ? 0xFFu : 0u));
   const uint32_t mR = ~(uint32_t)(0xFFull << (((uint32_t)min(tw, 5) << 3) - 8u));
+  if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);  // not needed under the W2 budget
+  uint32_t win[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int wi = wbit[t] >> 5;
+    const uint64_t both = ((uint64_t)whi[t] << 32) | (wi >= 0 ? wlo[t] : 0u);
+    win[t] = (uint32_t)(both >> (uint32_t)(wbit[t] - wi * 32)) & 0xFFFu;
+  }
+  const uint32_t own = win[0];
+  const uint32_t up = hasU ? win[1] : 0u, dn = hasD ? win[2] : 0u;
+  const uint32_t o_lo = onehot4(spread4(own)), o_hi = onehot4(spread4(own >> 8));
+  const uint32_t L = o_lo;                                     // x-1
+  const uint32_t O = __builtin_amdgcn_alignbyte(o_hi, o_lo, 1);  // x
+  const uint32_t R = __builtin_amdgcn_alignbyte(o_hi, o_lo, 2);  // x+1
+  const uint32_t U = onehot4(spread4(up >> 2)), Dn = onehot4(spread4(dn >> 2));
   if constexpr (MODE != FW_PROPOSE_CUTEDGE) {
     const uint32_t bits = (U & mU) | (L & mL) | (R & mR) | (Dn & mD);
     w4 = byte_popc(bits & ~O & mN);
@@ -268,11 +288,11 @@ __device__ __forceinline__ void weights4_swar(const LDS uint8_t* lab, int x0, in
 }
 
 // weights (and, when NEED_CD, cut degrees) of nodes x0..x0+3, one per byte
-template <int LB, int MODE, bool NEED_CD>
+template <int LB, int MODE, bool NEED_CD, bool BATCH = true>
 __device__ __forceinline__ void weights4x(const LDS uint8_t* lab, int x0, int W, int H, int n,
                                           GDiv gd, uint32_t& w4, uint32_t& cd4) {
   if constexpr (LB == 2)
-    weights4_swar<MODE, NEED_CD>(lab, x0, W, H, n, gd, w4, cd4);
+    weights4_swar<MODE, NEED_CD, BATCH>(lab, x0, W, H, n, gd, w4, cd4);
   else
     weights4<LB, MODE>(lab, x0, W, H, n, gd, w4, cd4);
 }
@@ -595,7 +615,7 @@ __device__ bool grid_race(const LDS uint8_t* lab, LDS uint8_t* scr, LDS uint32_t
 // trajectories, counters and sums stay bit-identical.  It raises the attempts per chain
 // per wave iteration (C3: 1.56 at R = 2, 2.05 at R = 4) where too few chains are left to
 // fill the GPU: an 8,192-chain shard leaves a third of the wave slots empty at R = 1.
-template <int LB, int MODE, int PER, bool FULL, bool BIG, int R>
+template <int LB, int MODE, int PER, bool FULL, bool BIG, int R, bool W2 = false>
 __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
   static_assert(PER % 2 == 0, "group sums are read as u16 pairs");
   static_assert(R == 1 || R == 2 || R == 4, "rows per chain");
@@ -1021,7 +1041,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       // ---- select, level 2: weights of the group's 64 nodes, 4 per lane
       const int x0 = gi * 64 + q * 4;
       uint32_t w4, cd4;  // four 8-bit weights
-      weights4x<LB, MODE, false>(lab, x0, W, H, n, gd, w4, cd4);
+      weights4x<LB, MODE, false, !W2>(lab, x0, W, H, n, gd, w4, cd4);
       // byte t: weights of nodes 0..t (<= 16); two shift-adds, not a quarter-rate multiply
       const uint32_t pref1 = w4 + (w4 << 8);
       const uint32_t pref = pref1 + (pref1 << 16);
@@ -1210,15 +1230,23 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
         // never a cell), so row ballot t is bits 16t .. 16t + 15 of A
         uint64_t A = 0;
         bool inw[4];
-        uint32_t lw[4];
+        uint32_t raw[4], lw[4];
+        int xw[4];
         const int wcol = q & 7;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {  // branch-free: all four reads issued, then masked
           const int wrow = 2 * t + (q >> 3);
           const int rr = vr + wrow - 3, cw = vc + wcol - 3;
           inw[t] = (wcol < 7) & (wrow < 7) & ((uint32_t)rr < (uint32_t)H) & ((uint32_t)cw < (uint32_t)W);
-          lw[t] = P::get(lab, inw[t] ? mulW(rr, W) + cw : v);
+          xw[t] = inw[t] ? mulW(rr, W) + cw : v;
+          raw[t] = lab[xw[t] >> 2];  // P::get's byte (2-bit labels) or nibble pair (4-bit)
+          if constexpr (LB != 2) raw[t] = P::get(lab, xw[t]);
         }
+        // the four loads stay together (one LDS round trip): at the register limit the
+        // scheduler otherwise put each load's wait before the next load
+        if constexpr (!W2) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) lw[t] = LB == 2 ? (raw[t] >> ((xw[t] & 3) << 1)) & 3u : raw[t];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           A |= (uint64_t)rowbits(ballot(inw[t] & (lw[t] == a)), row) << (ROW * t);
@@ -1589,7 +1617,7 @@ __global__ __launch_bounds__(64 * MAX_NW) __attribute__((amdgpu_waves_per_eu(3))
 }
 template <int LB, int MODE, int PER>
 __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_w2_kernel(FwRunParams p) {
-  grid16_body<LB, MODE, PER, false, false, 1>(p);
+  grid16_body<LB, MODE, PER, false, false, 1, true>(p);
 }
 
 // speculative attempts: R rows per chain.  A 3-waves-per-SIMD register budget (168 VGPRs:
