@@ -1568,9 +1568,13 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       // lane of a row holds the row-uniform values): 9 requests instead of 19 4- and 8-byte
       // ones (no measurable change in time or PMC WRITE_SIZE: profiles/r02/c3)
       if (q <= 8) {
-        uint64_t* rec = reinterpret_cast<uint64_t*>(stp);
-        const uint64_t o0 = rec[2 * q];
-        const uint64_t o1 = q < 8 ? rec[2 * q + 1] : 0ull;
+        // the record address from a lane id made opaque here: hoisted to the kernel entry,
+        // its 64-bit lane offset was the one value the 3-wave register budget spilled
+        int qw = q;
+        asm volatile("" : "+v"(qw));
+        uint64_t* rec = reinterpret_cast<uint64_t*>(stp) + 2 * qw;
+        const uint64_t o0 = rec[0];
+        const uint64_t o1 = qw < 8 ? rec[1] : 0ull;
         const uint64_t yinc = (uint64_t)n_steps + (first ? 1u : 0u);
         uint64_t w0, w1;
         switch (q) {
@@ -1587,11 +1591,11 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
             break;
           default: w0 = (uint64_t)(uint32_t)npairs | ((uint64_t)(uint32_t)stuck << 32); w1 = 0;
         }
-        if (q < 8) {
+        if (qw < 8) {
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-          *reinterpret_cast<u64x2*>(rec + 2 * q) = u64x2{w0, w1};
+          *reinterpret_cast<u64x2*>(rec) = u64x2{w0, w1};
         } else {
-          rec[16] = w0;
+          rec[0] = w0;
         }
       }
     }
@@ -1613,7 +1617,14 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
 // waves of work per SIMD (the 8-GPU job's 8,192-chain shards: +4.6%).
 template <int LB, int MODE, int PER, bool FULL, bool BIG>
 __global__ __launch_bounds__(64 * MAX_NW) __attribute__((amdgpu_waves_per_eu(3))) void fw_grid16_kernel(FwRunParams p) {
+  static_assert(!FULL, "FULL instantiations: fw_grid16_full_kernel");
   grid16_body<LB, MODE, PER, FULL, BIG, 1>(p);
+}
+// FULL (optional features on): the compiler's own register budget, as in round 5 (held to 3
+// waves per SIMD it spilled 130-190 B per lane)
+template <int LB, int MODE, int PER, bool FULL, bool BIG>
+__global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_full_kernel(FwRunParams p) {
+  grid16_body<LB, MODE, PER, true, BIG, 1>(p);
 }
 template <int LB, int MODE, int PER>
 __global__ __launch_bounds__(64 * MAX_NW) void fw_grid16_w2_kernel(FwRunParams p) {
@@ -1638,6 +1649,14 @@ int per16(int G) { return G <= 16 * 2 ? 2 : G <= 16 * 4 ? 4 : G <= 16 * 10 ? 10 
 int per16_big(int G) { return (G + 15) / 16 <= 32 ? 2 : 4; }
 bool is_big(int G) { return G > 16 * 16; }
 
+template <int LB, int MODE, int PER, bool FULL, bool BIG>
+void* k16() {
+  if constexpr (FULL)
+    return reinterpret_cast<void*>(&fw_grid16_full_kernel<LB, MODE, PER, true, BIG>);
+  else
+    return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, PER, false, BIG>);
+}
+
 template <int LB, int MODE, bool FULL>
 void* pick16(int G) {
   if (is_big(G)) {
@@ -1645,18 +1664,18 @@ void* pick16(int G) {
       return nullptr;  // large grids take 2- or 3-bit labels
     } else {
       return per16_big(G) == 2
-                 ? reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL, true>)
-                 : reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL, true>);
+                 ? k16<LB, MODE, 2, FULL, true>()
+                 : k16<LB, MODE, 4, FULL, true>();
     }
   }
   if constexpr (LB == 3) {
     return nullptr;  // small grids keep 2- or 4-bit labels
   } else {
     switch (per16(G)) {
-      case 2: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 2, FULL, false>);
-      case 4: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 4, FULL, false>);
-      case 10: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 10, FULL, false>);
-      default: return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, 16, FULL, false>);
+      case 2: return k16<LB, MODE, 2, FULL, false>();
+      case 4: return k16<LB, MODE, 4, FULL, false>();
+      case 10: return k16<LB, MODE, 10, FULL, false>();
+      default: return k16<LB, MODE, 16, FULL, false>();
     }
   }
 }
