@@ -723,17 +723,24 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
     const uint64_t gid = (uint64_t)(p.chain_id0 + c);
     const bool cached = p.gcache_ok != 0 || seg > 0;  // derived-state cache (FwRunParams)
 
-    // ---- load state (each row loads its own chain)
+    // ---- load state (each row loads its own chain).  OPQ: the record addresses, here and
+    // at the write-back, from an opaque lane id; hoisted to the kernel entry, their 64-bit
+    // lane offsets were what the register budget spilled in the speculative and cut-edge
+    // instantiations (12-28 B of scratch per lane).  Not in the pairs kernels, which do not
+    // spill and lose 0.4% (C3) to the recomputation.
+    constexpr bool OPQ = R > 1 || MODE == FW_PROPOSE_CUTEDGE;
+    int ql = q;
+    if constexpr (OPQ) asm volatile("" : "+v"(ql));
     {
       const u32x4* src = reinterpret_cast<const u32x4*>(p.labels + (size_t)cc * p.lab_stride);
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(lab);
       // with a valid derived-state cache the slot's group sums come along (see lab_copy16)
       const int nv = cached ? p.lab_copy16 : p.lab_bytes / 16;
-      for (int i = sx * ROW + q; i < nv; i += R * ROW) dst[i] = src[i];
+      for (int i = sx * ROW + ql; i < nv; i += R * ROW) dst[i] = src[i];
     }
-    int32_t pops = q < k ? (int32_t)p.pops[(size_t)cc * k + q] : 0;  // total pop < 2^31
-    double thr_l = FULL && q < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + q] : 0.0;
-    uint64_t thr53_l = q < 2 * D + 1 ? p.thr53[(size_t)cc * p.thr_stride + q] : 0ull;
+    int32_t pops = ql < k ? (int32_t)p.pops[(size_t)cc * k + ql] : 0;  // total pop < 2^31
+    double thr_l = FULL && ql < 2 * D + 1 ? p.thr[(size_t)cc * p.thr_stride + ql] : 0.0;
+    uint64_t thr53_l = ql < 2 * D + 1 ? p.thr53[(size_t)cc * p.thr_stride + ql] : 0ull;
     fw_chain_stats* stp = p.stats + cc;
     const uint64_t acc0 = FULL && p.sched ? stp->accepts : 0ull;
     // scheduled bounds: the row of the next proposal's step_num (accepted flips + 1)
@@ -769,7 +776,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
     uint32_t bpos_w = ROW * R;  // R > 1: next unconsumed attempt of the group's Philox batch
     Pend pend = maps_on ? pend_load(p, cc) : Pend{-1, 0, 0u};
     // boundary_node-flagged nodes of district q (FW_ACCEPT_BOUNDARY), lane q
-    int32_t bcnt = rule == FW_ACCEPT_BOUNDARY && q < k ? p.bcnt[(size_t)cc * k + q] : 0;
+    int32_t bcnt = rule == FW_ACCEPT_BOUNDARY && ql < k ? p.bcnt[(size_t)cc * k + ql] : 0;
     lds_order();
 
     // ---- derive group sums, cut / boundary / proposal-set counts (per row), unless the
@@ -1554,11 +1561,13 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       if (hb0) HIST_ADD(p.hist_b + base_b + q, (unsigned long long)hb0);
       if (hb1) HIST_ADD(p.hist_b + base_b + ROW + q, (unsigned long long)hb1);
       if (FULL && RN && q == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
+      int qw = q;  // OPQ: see the state load
+      if constexpr (OPQ) asm volatile("" : "+v"(qw));
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(lab);
-      for (int i = q; i < p.lab_copy16; i += ROW) dst[i] = src[i];  // labels + group sums
-      if (q < k) p.pops[(size_t)c * k + q] = (int64_t)pops;
-      if (q < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + q] = bcnt;
+      for (int i = qw; i < p.lab_copy16; i += ROW) dst[i] = src[i];  // labels + group sums
+      if (qw < k) p.pops[(size_t)c * k + qw] = (int64_t)pops;
+      if (qw < k && rule == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + qw] = bcnt;
       if (q == 0 && maps_on) pend_store(p, c, pend);
       if (q == 0 && waits_on) {
         p.wsamp[2 * (size_t)c] = wsum;
@@ -1568,13 +1577,13 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
       // lane of a row holds the row-uniform values): 9 requests instead of 19 4- and 8-byte
       // ones (no measurable change in time or PMC WRITE_SIZE: profiles/r02/c3)
       if (q <= 8) {
-        // the record address from a lane id made opaque here: hoisted to the kernel entry,
-        // its 64-bit lane offset was the one value the 3-wave register budget spilled
-        int qw = q;
-        asm volatile("" : "+v"(qw));
-        uint64_t* rec = reinterpret_cast<uint64_t*>(stp) + 2 * qw;
+        // the record address from an opaque lane id in every instantiation: hoisted, its
+        // 64-bit lane offset was the one value the C3 kernel's 3-wave budget spilled
+        int qr = qw;
+        if constexpr (!OPQ) asm volatile("" : "+v"(qr));
+        uint64_t* rec = reinterpret_cast<uint64_t*>(stp) + 2 * qr;
         const uint64_t o0 = rec[0];
-        const uint64_t o1 = qw < 8 ? rec[1] : 0ull;
+        const uint64_t o1 = qr < 8 ? rec[1] : 0ull;
         const uint64_t yinc = (uint64_t)n_steps + (first ? 1u : 0u);
         uint64_t w0, w1;
         switch (q) {
@@ -1591,7 +1600,7 @@ __device__ __forceinline__ void grid16_body(const FwRunParams& p) {
             break;
           default: w0 = (uint64_t)(uint32_t)npairs | ((uint64_t)(uint32_t)stuck << 32); w1 = 0;
         }
-        if (qw < 8) {
+        if (qr < 8) {
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
           *reinterpret_cast<u64x2*>(rec) = u64x2{w0, w1};
         } else {

@@ -116,14 +116,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // ---- load state (with a valid derived-state cache the group sums that follow the
     // labels in the chain's record come along: FwRunParams::lab_copy16)
     const bool cached = p.gcache_ok != 0 || seg > 0;
+    // the per-lane addresses of the chain's records from an opaque lane id, here and at the
+    // write-back: hoisted to the kernel entry they were 64-bit pointers held across the unit
+    // loop, and spilled (C4 20 B, C5 28 B of scratch per lane)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     {
       const u32x4* src = reinterpret_cast<const u32x4*>(p.labels + (size_t)c * p.lab_stride);
       LDS u32x4* dst = reinterpret_cast<LDS u32x4*>(C.lab);
       const int nv = cached ? p.lab_copy16 : p.lab_bytes / 16;
-      for (int i = lane; i < nv; i += WAVE) dst[i] = src[i];
+      for (int i = ln; i < nv; i += WAVE) dst[i] = src[i];
     }
-    int64_t pops = lane < k ? p.pops[(size_t)c * k + lane] : 0;  // lane d holds district d
-    double thr_l = lane < 2 * D + 1 ? p.thr[(size_t)c * p.thr_stride + lane] : 0.0;
+    int64_t pops = ln < k ? p.pops[(size_t)c * k + ln] : 0;  // lane d holds district d
+    double thr_l = ln < 2 * D + 1 ? p.thr[(size_t)c * p.thr_stride + ln] : 0.0;
     fw_chain_stats* stp = p.stats + c;
     const uint64_t acc0 = FULL && p.sched ? rfl64(stp->accepts) : 0ull;
     // scheduled bounds: the row of the next proposal's step_num (accepted flips + 1)
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     uint64_t n_bfs = in_vgpr64(0), n_bfsn = in_vgpr64(0), n_bfsd = in_vgpr64(0);
     Pend pend = FULL ? pend_load(p, c) : Pend{-1, 0, 0u};
     // boundary_node-flagged nodes of district `lane` (FW_ACCEPT_BOUNDARY)
-    int32_t bcnt = FULL && p.accept == FW_ACCEPT_BOUNDARY && lane < k ? p.bcnt[(size_t)c * k + lane] : 0;
+    int32_t bcnt = FULL && p.accept == FW_ACCEPT_BOUNDARY && ln < k ? p.bcnt[(size_t)c * k + ln] : 0;
     __syncthreads();
 
     // ---- derive group sums, cut count, boundary count, proposal-set size (unless cached)
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     } else {
       uint32_t cut2 = 0, bn = 0, np = 0;
       if constexpr (WB) {
-        for (int i = lane; i < (n + 15) / 16; i += WAVE) C.wts[i] = 0u;
+        for (int i = ln; i < (n + 15) / 16; i += WAVE) C.wts[i] = 0u;
         lds_order();
       }
       for (int t = 0; t < G; ++t) {
@@ -472,11 +477,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (hb) atomicAdd(p.hist_b + base_b + lane, (unsigned long long)hb);
     if (RN && lane == 0 && rrun) atomicAdd(p.hist_ring + rpair, (unsigned long long)rrun);
     {
+      int lw = lane;
+      asm volatile("" : "+v"(lw));
       u32x4* dst = reinterpret_cast<u32x4*>(p.labels + (size_t)c * p.lab_stride);
       const LDS u32x4* src = reinterpret_cast<const LDS u32x4*>(C.lab);
-      for (int i = lane; i < p.lab_copy16; i += WAVE) dst[i] = src[i];  // labels + group sums
-      if (lane < k) p.pops[(size_t)c * k + lane] = pops;
-      if (FULL && lane < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lane] = bcnt;
+      for (int i = lw; i < p.lab_copy16; i += WAVE) dst[i] = src[i];  // labels + group sums
+      if (lw < k) p.pops[(size_t)c * k + lw] = pops;
+      if (FULL && lw < k && p.accept == FW_ACCEPT_BOUNDARY) p.bcnt[(size_t)c * k + lw] = bcnt;
     }
     if (FULL && lane == 0 && p.m_acc != nullptr) pend_store(p, c, pend);
     if (waits_on && lane == 0) {
