@@ -71,7 +71,7 @@ run_task() {
     prof_c5fresh) prof c5fresh "--config c5 --shard 0/8" ;;
     profile:*)  # profile:TAG:BENCH_ARGS (',' for ' '): profile.sh passes of exactly that protocol
       local r=${t#profile:}; local tag=${r%%:*}; local a=${r#*:}; a=${a//,/ }
-      BENCH_ARGS="$a --no-cpu-baseline --check-chains 0" timeout -k 10 1100 bash scripts/profile.sh $tag > "$O/prof_$tag.log" 2>&1 \
+      BENCH_ARGS="$a --no-cpu-baseline --check-chains 0 --secondary-inner 0" timeout -k 10 1100 bash scripts/profile.sh $tag > "$O/prof_$tag.log" 2>&1 \
         || { echo "profile $tag failed"; tail -20 "$O/prof_$tag.log"; return 1; }
       grep -E "traffic ->|timed=" "$O/prof_$tag.log" ;;
     prof_c4) prof c4 "--config c4" ;;
@@ -129,7 +129,7 @@ run_task() {
         done
       done ;;
     shards_c5)  # the 8-GPU C5 job emulated shard by shard at the steady-state protocol
-      timeout -k 10 900 bash scripts/shards.sh 8 "--config c5 --inner 5000 --steps 20 --warmup 2 --check-chains 2" c5 > $O/shards_c5.log 2>&1 || { tail -5 $O/shards_c5.log; return 1; }
+      timeout -k 10 900 bash scripts/shards.sh 8 "--config c5 --steps 20 --warmup 5 --check-chains 2" c5 > $O/shards_c5.log 2>&1 || { tail -5 $O/shards_c5.log; return 1; }
       tail -10 $O/shards_c5.log ;;
     shards_c3)  # the 8-GPU C3 job emulated shard by shard on the driver protocol
       timeout -k 10 600 bash scripts/shards.sh 8 "--config c3 --steps 20 --warmup 5 --check-chains 2" c3 > $O/shards_c3.log 2>&1 || { tail -5 $O/shards_c3.log; return 1; }

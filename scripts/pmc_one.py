@@ -7,7 +7,7 @@ import json
 import re
 import sys
 
-CHAIN_KERNEL = re.compile(r"fw_(grid16|grid16_spec|run)_kernel")
+CHAIN_KERNEL = re.compile(r"fw_(grid16|grid16_spec|grid16_w2|grid16_full|run)_kernel")
 d, k = sys.argv[1], int(sys.argv[2])
 per = collections.defaultdict(dict)
 name = None

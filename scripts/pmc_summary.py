@@ -21,7 +21,7 @@ import os
 import re
 import sys
 
-CHAIN_KERNEL = re.compile(r"fw_(grid16|grid16_spec|run)_kernel")
+CHAIN_KERNEL = re.compile(r"fw_(grid16|grid16_spec|grid16_w2|grid16_full|run)_kernel")
 
 d = sys.argv[1]
 

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r01}
 shift
 CFG_ARGS=${CFG_ARGS:-}   # e.g. "--config c5" (default: the C3 bench line)
-BENCH_ARGS=${BENCH_ARGS:-"--steps 20 --warmup 5 --inner 1000 --no-cpu-baseline --check-chains 0 $CFG_ARGS"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 20 --warmup 5 --no-cpu-baseline --check-chains 0 --secondary-inner 0 $CFG_ARGS"}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
