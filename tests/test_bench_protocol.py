@@ -31,3 +31,31 @@ def test_pmc_mismatch_accepts_only_the_same_run():
     assert "grid" in bench.pmc_mismatch(prof, _ident(grid=40), 15.2)
     assert "no PMC profile" in bench.pmc_mismatch(None, _ident(), 15.2)
     assert "no identity" in bench.pmc_mismatch({"source": "old"}, _ident(), 15.2)
+
+
+def test_committed_profiles_match_the_in_tree_library():
+    """Every stored profile is named by its own protocol and was taken with the library the
+    tree ships, so the driver's lines use it: a kernel change without re-profiling fails
+    here (on CPU), not silently as ``pmc.used: false`` in the round's bench line.  The
+    driver's protocol (``--steps 20 --warmup 5``, C3, default launch length) must be among
+    them."""
+    import glob
+    import json
+    import os
+    from flipcomplexityempirical_amd._lib import build_info
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "profiles", "pmc", "*.json")))
+    assert files, "no PMC profiles under profiles/pmc"
+    build = build_info()
+    for f in files:
+        prof = json.load(open(f))
+        ident = prof["identity"]
+        key = bench.pmc_key(ident["config"], ident["order"], ident["chains"], ident["inner"],
+                            ident["warmup"], ident["steps"], ident["chain_id0"],
+                            ident["resumed_steps"])
+        assert os.path.basename(f) == key + ".json", f
+        assert ident["build"] == build, f"{f}: profiled build {ident['build']!r}, tree {build!r}"
+        assert ident["flipwalk_env"] == {}, f
+    keys = {os.path.basename(f)[:-5] for f in files}
+    assert bench.pmc_key("c3", None, 65536, 5000, 5, 20) in keys
