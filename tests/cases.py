@@ -70,6 +70,11 @@ def cases(include_kansas: bool = True):
         Case("grid7x9_k3_cut", grid_graph(7, 9), band_seed(7, 9, 3), 3, 2, 0.30, 0.7),
         Case("grid11x13_k4", grid_graph(11, 13), band_seed(11, 13, 4), 4, 1, 0.30, MU),
         Case("grid30x18_k2_bi", grid_graph(30, 18), band_seed(30, 18, 2), 2, 0, 0.10, 0.4),
+        # edge shapes: the narrowest grid of the four-chains-per-wave kernel (W = 4), one
+        # below it (W = 3: the one-chain-per-wave kernel on the grid), three rows only
+        Case("grid40x4_k2", grid_graph(40, 4), band_seed(40, 4, 2), 2, 1, 0.20, 0.8),
+        Case("grid40x3_k2_cut", grid_graph(40, 3), band_seed(40, 3, 2), 2, 2, 0.20, MU),
+        Case("grid3x40_k2_bi", grid_graph(3, 40), band_seed(3, 40, 2), 2, 0, 0.40, 0.6),
     ]
     g11 = sec11_graph()
     out.append(Case("sec11_a2_k2", g11, sec11_seed(g11, 2), 2, 0, 0.05, 0.1))
