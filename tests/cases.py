@@ -55,6 +55,24 @@ class Case:
         return metropolis_table(self.base, self.graph.maxdeg)
 
 
+def hub_graph(n: int = 15) -> Graph:
+    """An n x n grid plus two hub nodes: one joined to every cell of the two middle rows
+    (degree 2n = 30), one to the middle column and to seven cells of row 0 (degree 22), so
+    the graph has no 16-wide padded-row table and runs the CSR-walking chain kernel."""
+    import networkx as nx
+    G = nx.grid_2d_graph(n, n)
+    G.add_node("hub")
+    for c in range(n):
+        G.add_edge("hub", (n // 2, c))
+        G.add_edge("hub", (n // 2 + 1, c))
+    G.add_node("hub2")
+    for r in range(n):
+        G.add_edge("hub2", (r, n // 2))
+    for c in range(7):
+        G.add_edge("hub2", (0, c))
+    return Graph.from_networkx(G)
+
+
 def c4_seed(g: Graph, k: int, percent: float = 0.05) -> np.ndarray:
     return tree_seed(g, k, percent)
 
@@ -84,6 +102,12 @@ def cases(include_kansas: bool = True):
     out.append(Case("frank_a0_k2_cold", gf, frankenstein_seed(gf, 0), 2, 0, 0.1, 0.3))
     gd = delaunay_graph(3000, seed=1)
     out.append(Case("delaunay3k_k18", gd, c4_seed(gd, 18), 18, 1, 0.05, MU))
+    # k = 31: every 5-bit label code but one in use
+    out.append(Case("delaunay3k_k31", gd, c4_seed(gd, 31, 0.10), 31, 1, 0.10, MU))
+    # hubs of degree 30 and 22: rows past the 16-wide padded table, the CSR-walking kernel
+    gh = hub_graph()
+    out.append(Case("hub_k3", gh, c4_seed(gh, 3, 0.10), 3, 1, 0.10, 1.2))
+    out.append(Case("hub_k2_cut", gh, c4_seed(gh, 2, 0.10), 2, 2, 0.10, MU))
     if include_kansas:
         out.append(Case("county_k2", kansas("County20"), kansas_seed("County20", 2), 2, 0, 0.10,
                         1.0))
