@@ -286,7 +286,7 @@ def boundary_flags(g: Graph) -> np.ndarray:
     the outer ring of the grid; Frankenstein_chain.py:259-265 the Frankengraph rim)."""
     if g.node_attrs is not None and g.node_attrs and "boundary_node" in g.node_attrs[0]:
         return np.array([1 if a["boundary_node"] else 0 for a in g.node_attrs], np.uint8)
-    if g.nodes and isinstance(g.nodes[0], tuple):
+    if g.nodes and all(isinstance(k, tuple) and len(k) == 2 for k in g.nodes):
         xs = np.array([k[0] for k in g.nodes])
         ys = np.array([k[1] for k in g.nodes])
         return ((xs == xs.min()) | (xs == xs.max()) | (ys == ys.min()) |

@@ -70,6 +70,8 @@ def hub_graph(n: int = 15) -> Graph:
         G.add_edge("hub2", (r, n // 2))
     for c in range(7):
         G.add_edge("hub2", (0, c))
+    for v in G.nodes:  # the grid's outer ring (boundary_condition); the hubs are interior
+        G.nodes[v]["boundary_node"] = isinstance(v, tuple) and (min(v) == 0 or max(v) == n - 1)
     return Graph.from_networkx(G)
 
 

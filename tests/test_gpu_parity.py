@@ -190,7 +190,8 @@ def test_grid_kernel_register_budgets(gpu_lib, name, w2, bitboard, monkeypatch):
 
 @pytest.mark.parametrize("name,path", [("grid20_k4_mu", "auto"), ("grid20_k4_mu", "wave64"),
                                        ("grid30x18_k2_bi", "auto"), ("sec11_a2_k2", "auto"),
-                                       ("tract_k4", "auto")])
+                                       ("tract_k4", "auto"), ("hub_k3", "auto"),
+                                       ("grid40x4_k2", "auto")])
 def test_search_list_spill(gpu_lib, name, path, monkeypatch):
     """A 2-entry LDS visit list: every exact search spills to its HBM slice (the grid
     kernel's bitboard search is switched off so that its list search runs)."""
@@ -209,7 +210,8 @@ ACCEPT_CASES = [("grid12_k4_pairs", "bratio", "auto"), ("grid20_k4_mu", "bratio"
                 ("grid16x24_k8", "bratio", "auto"), ("sec11_a2_k2", "bratio", "auto"),
                 ("tract_k4", "bratio", "auto"), ("grid10_k2_bi", "boundary", "auto"),
                 ("grid30x18_k2_bi", "boundary", "wave64"), ("sec11_a0_k2_mu", "boundary", "auto"),
-                ("frank_a2_k2", "boundary", "auto"), ("grid12_k4_cut", "boundary", "auto")]
+                ("frank_a2_k2", "boundary", "auto"), ("grid12_k4_cut", "boundary", "auto"),
+                ("hub_k3", "bratio", "auto"), ("hub_k2_cut", "boundary", "auto")]
 
 
 @pytest.mark.parametrize("name,rule,path", ACCEPT_CASES,

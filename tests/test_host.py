@@ -175,3 +175,20 @@ def test_hilbert_numbering_is_the_same_graph():
     xy = np.array([[(i + .5) / side, (j + .5) / side] for i in range(side) for j in range(side)])
     walk = (xy[np.argsort(hilbert_index(xy, 2))] * side).astype(int)
     assert all(np.abs(walk[i] - walk[i + 1]).sum() == 1 for i in range(15))
+
+
+def test_boundary_flags_needs_attributes_or_coordinate_keys():
+    """boundary_condition's flags come from the boundary_node attribute, else from (x, y)
+    keys; a graph with neither (or with keys of mixed kinds) is refused by name."""
+    import networkx as nx
+    import pytest as _pytest
+    from flipcomplexityempirical_amd.graph import Graph, boundary_flags
+    G = nx.grid_2d_graph(3, 4)
+    f = boundary_flags(Graph.from_networkx(G))
+    assert f.sum() == 10 and f[[k for k in G.nodes].index((1, 1))] == 0
+    G.add_edge("hub", (1, 1))
+    with _pytest.raises(ValueError, match="boundary_node"):
+        boundary_flags(Graph.from_networkx(G))
+    for v in G.nodes:
+        G.nodes[v]["boundary_node"] = v == "hub"
+    assert boundary_flags(Graph.from_networkx(G)).sum() == 1
