@@ -19,7 +19,8 @@ pytestmark = pytest.mark.gpu
 CASES = {c.name: c for c in cases()}
 MAP_CASES = [("grid12_k4_pairs", "auto"), ("grid16x24_k8", "auto"), ("grid10_k2_bi", "auto"),
              ("grid7x9_k3_cut", "auto"), ("grid20_k4_mu", "wave64"), ("sec11_a2_k2", "auto"),
-             ("frank_a2_k2", "auto"), ("tract_k4", "auto"), ("delaunay3k_k18", "auto")]
+             ("frank_a2_k2", "auto"), ("tract_k4", "auto"), ("delaunay3k_k18", "auto"),
+             ("hub_k3", "auto"), ("grid40x4_k2", "auto")]
 
 
 def label_values(k):
