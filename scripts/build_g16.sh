@@ -9,7 +9,7 @@ CS=${SRC_DIR:-$ROOT/flipcomplexityempirical_amd/csrc}
 B=$ROOT/flipcomplexityempirical_amd/csrc/build
 OUT=/tmp/fwg16_$NAME; mkdir -p $OUT $ROOT/ab
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS"
-/opt/rocm/bin/hipcc $F -c -o $OUT/fw_grid16.o $CS/fw_grid16.hip
+/opt/rocm/bin/hipcc $F ${GRID16_FLAGS--mllvm -amdgpu-sched-strategy=max-ilp} -c -o $OUT/fw_grid16.o $CS/fw_grid16.hip
 (cd $ROOT/flipcomplexityempirical_amd/csrc && ./gen_build_info.sh $OUT/build_info.cpp "$F g16:$NAME")
 g++ -O2 -fPIC -c -o $OUT/build_info.o $OUT/build_info.cpp
 /opt/rocm/bin/hipcc $F -shared -o $ROOT/ab/lib_$NAME.so $B/fw_api.o $B/fw_kernels.o $OUT/fw_grid16.o $OUT/build_info.o
