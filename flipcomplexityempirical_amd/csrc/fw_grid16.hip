@@ -1735,6 +1735,17 @@ int round16i(int x) { return (x + 15) / 16 * 16; }
 
 }  // namespace
 
+// The W2 instantiations live in a translation unit of their own (fw_grid16_w2.hip includes
+// this file with FW_G16_W2_TU), so the Makefile can schedule them differently from the
+// 3-wave ones; the stamps build keeps them here.
+void* fw_grid16_pick_w2(int mode, int G);
+#if defined(FW_G16_W2_TU) || defined(FW_STAMPS)
+void* fw_grid16_pick_w2(int mode, int G) {
+  return mode == FW_PROPOSE_CUTEDGE ? pick16_w2<FW_PROPOSE_CUTEDGE>(G) : pick16_w2<FW_PROPOSE_PAIRS>(G);
+}
+#endif
+#ifndef FW_G16_W2_TU
+
 #ifdef FW_STAMPS
 extern "C" int fw_debug_unit_times(unsigned long long* out, int n) {
   if (n > 65536) return -1;
@@ -1788,8 +1799,7 @@ int fw_grid16_launch_nw(const FwRunParams& p) { return p.nw * fw_grid16_launch_r
 // the W2 instantiation (2-bit labels, small grids, lean, R = 1)
 static void* grid16_fn_w2(const FwRunParams& p) {
   if (p.lb != 2) return nullptr;
-  return p.mode == FW_PROPOSE_CUTEDGE ? pick16_w2<FW_PROPOSE_CUTEDGE>(p.G)
-                                      : pick16_w2<FW_PROPOSE_PAIRS>(p.G);
+  return fw_grid16_pick_w2(p.mode, p.G);
 }
 
 static void* grid16_fn_r(const FwRunParams& p, bool full, int R) {
@@ -1982,3 +1992,4 @@ int fw_grid16_launch(const FwRunParams& p, int grid, void* stream) {
   return (int)hipLaunchKernel(fn, dim3(grid), dim3(64 * fw_grid16_launch_nw(p)), args,
                               (size_t)p.lds16, (hipStream_t)stream);
 }
+#endif  // FW_G16_W2_TU
