@@ -78,6 +78,12 @@ static_assert(offsetof(fw_chain_stats, yields) == 88 && offsetof(fw_chain_stats,
 
 #define HIST_ADD(ptr, v) atomicAdd(ptr, v)
 
+// Pickers of the instantiations compiled in their own translation units (the Makefile
+// schedules each differently): fw_grid16_lean.hip the small-grid lean kernels,
+// fw_grid16_w2.hip the W2 ones.  The stamps build compiles everything here.
+void* fw_grid16_pick_lean(int lb, int mode, int G);
+void* fw_grid16_pick_w2(int mode, int G);
+
 namespace {
 
 constexpr int ROW = 16;
@@ -1666,6 +1672,17 @@ void* k16() {
     return reinterpret_cast<void*>(&fw_grid16_kernel<LB, MODE, PER, false, BIG>);
 }
 
+// the small-grid lean instantiations (fw_grid16_lean.hip; the stamps build: here)
+template <int LB, int MODE>
+void* pick16_small_lean(int G) {
+  switch (per16(G)) {
+    case 2: return k16<LB, MODE, 2, false, false>();
+    case 4: return k16<LB, MODE, 4, false, false>();
+    case 10: return k16<LB, MODE, 10, false, false>();
+    default: return k16<LB, MODE, 16, false, false>();
+  }
+}
+
 template <int LB, int MODE, bool FULL>
 void* pick16(int G) {
   if (is_big(G)) {
@@ -1679,13 +1696,19 @@ void* pick16(int G) {
   }
   if constexpr (LB == 3) {
     return nullptr;  // small grids keep 2- or 4-bit labels
-  } else {
+  } else if constexpr (FULL) {
     switch (per16(G)) {
-      case 2: return k16<LB, MODE, 2, FULL, false>();
-      case 4: return k16<LB, MODE, 4, FULL, false>();
-      case 10: return k16<LB, MODE, 10, FULL, false>();
-      default: return k16<LB, MODE, 16, FULL, false>();
+      case 2: return k16<LB, MODE, 2, true, false>();
+      case 4: return k16<LB, MODE, 4, true, false>();
+      case 10: return k16<LB, MODE, 10, true, false>();
+      default: return k16<LB, MODE, 16, true, false>();
     }
+  } else {
+#if defined(FW_STAMPS)
+    return pick16_small_lean<LB, MODE>(G);
+#else
+    return fw_grid16_pick_lean(LB, MODE, G);  // fw_grid16_lean.hip
+#endif
   }
 }
 
@@ -1735,16 +1758,23 @@ int round16i(int x) { return (x + 15) / 16 * 16; }
 
 }  // namespace
 
-// The W2 instantiations live in a translation unit of their own (fw_grid16_w2.hip includes
-// this file with FW_G16_W2_TU), so the Makefile can schedule them differently from the
-// 3-wave ones; the stamps build keeps them here.
-void* fw_grid16_pick_w2(int mode, int G);
+// fw_grid16_w2.hip and fw_grid16_lean.hip include this file with FW_G16_W2_TU /
+// FW_G16_LEAN_TU and compile only their pickers' instantiations
 #if defined(FW_G16_W2_TU) || defined(FW_STAMPS)
 void* fw_grid16_pick_w2(int mode, int G) {
   return mode == FW_PROPOSE_CUTEDGE ? pick16_w2<FW_PROPOSE_CUTEDGE>(G) : pick16_w2<FW_PROPOSE_PAIRS>(G);
 }
 #endif
-#ifndef FW_G16_W2_TU
+#if defined(FW_G16_LEAN_TU) || defined(FW_STAMPS)
+void* fw_grid16_pick_lean(int lb, int mode, int G) {
+  const bool cut = mode == FW_PROPOSE_CUTEDGE;
+  if (is_big(G)) return nullptr;  // fw_grid16.hip's large-grid plan
+  if (lb == 2) return cut ? pick16_small_lean<2, FW_PROPOSE_CUTEDGE>(G) : pick16_small_lean<2, FW_PROPOSE_PAIRS>(G);
+  if (lb == 4) return cut ? pick16_small_lean<4, FW_PROPOSE_CUTEDGE>(G) : pick16_small_lean<4, FW_PROPOSE_PAIRS>(G);
+  return nullptr;
+}
+#endif
+#if !defined(FW_G16_W2_TU) && !defined(FW_G16_LEAN_TU)
 
 #ifdef FW_STAMPS
 extern "C" int fw_debug_unit_times(unsigned long long* out, int n) {
@@ -1992,4 +2022,4 @@ int fw_grid16_launch(const FwRunParams& p, int grid, void* stream) {
   return (int)hipLaunchKernel(fn, dim3(grid), dim3(64 * fw_grid16_launch_nw(p)), args,
                               (size_t)p.lds16, (hipStream_t)stream);
 }
-#endif  // FW_G16_W2_TU
+#endif  // !FW_G16_W2_TU && !FW_G16_LEAN_TU

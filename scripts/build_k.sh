@@ -12,5 +12,5 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS"
 /opt/rocm/bin/hipcc $F -c -o $OUT/fw_kernels.o $CS/fw_kernels.hip
 (cd $ROOT/flipcomplexityempirical_amd/csrc && ./gen_build_info.sh $OUT/build_info.cpp "$F k:$NAME")
 g++ -O2 -fPIC -c -o $OUT/build_info.o $OUT/build_info.cpp
-/opt/rocm/bin/hipcc $F -shared -o $ROOT/ab/lib_$NAME.so $B/fw_api.o $OUT/fw_kernels.o $B/fw_grid16.o $B/fw_grid16_w2.o $OUT/build_info.o
+/opt/rocm/bin/hipcc $F -shared -o $ROOT/ab/lib_$NAME.so $B/fw_api.o $OUT/fw_kernels.o $B/fw_grid16.o $B/fw_grid16_lean.o $B/fw_grid16_w2.o $OUT/build_info.o
 echo built ab/lib_$NAME.so

@@ -22,10 +22,11 @@ cd $SRC/flipcomplexityempirical_amd/csrc
 OUT=/tmp/fwvar_$NAME; mkdir -p $OUT
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS"
 for s in fw_api fw_kernels; do /opt/rocm/bin/hipcc $F -c -o $OUT/$s.o $s.hip & done
-/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=iterative-ilp -c -o $OUT/fw_grid16.o fw_grid16.hip &
+/opt/rocm/bin/hipcc $F -c -o $OUT/fw_grid16.o fw_grid16.hip &
+/opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=iterative-ilp -c -o $OUT/fw_grid16_lean.o fw_grid16_lean.hip &
 /opt/rocm/bin/hipcc $F -mllvm -amdgpu-sched-strategy=max-ilp -c -o $OUT/fw_grid16_w2.o fw_grid16_w2.hip &
 wait
 ./gen_build_info.sh $OUT/build_info.cpp "$F$TAGS"
 g++ -O2 -fPIC -c -o $OUT/build_info.o $OUT/build_info.cpp
-/opt/rocm/bin/hipcc $F -shared -o $ROOT/ab/lib_$NAME.so $OUT/fw_api.o $OUT/fw_kernels.o $OUT/fw_grid16.o $OUT/fw_grid16_w2.o $OUT/build_info.o
+/opt/rocm/bin/hipcc $F -shared -o $ROOT/ab/lib_$NAME.so $OUT/fw_api.o $OUT/fw_kernels.o $OUT/fw_grid16.o $OUT/fw_grid16_lean.o $OUT/fw_grid16_w2.o $OUT/build_info.o
 echo built ab/lib_$NAME.so

@@ -46,7 +46,8 @@ def test_build_info_names_sources_and_flags():
     assert "--offload-arch=gfx950" in m.group(2)
     csrc = os.path.join(ROOT, "flipcomplexityempirical_amd", "csrc")
     blob = b"".join(open(os.path.join(csrc, f), "rb").read() for f in
-                    ("fw_api.hip", "fw_kernels.hip", "fw_grid16.hip", "fw_grid16_w2.hip",
+                    ("fw_api.hip", "fw_kernels.hip", "fw_grid16.hip", "fw_grid16_lean.hip",
+                     "fw_grid16_w2.hip",
                      "fw_internal.h", "fw_device.h", "fw_math.h"))
     blob += open(os.path.join(ROOT, "include", "flipwalk.h"), "rb").read()
     assert m.group(1) == hashlib.sha256(blob).hexdigest()[:16], "library older than its sources"
